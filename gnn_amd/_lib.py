@@ -1,0 +1,68 @@
+"""ctypes binding of libgnn_spmm.so (the C ABI declared in include/gnn_spmm.h).
+
+The shared library is built in-tree by ``gnn_amd.build.build_library()`` (hipcc,
+--offload-arch=gfx950) and travels with the repository snapshot. There is deliberately no
+fallback: if the library is missing or fails to load, every operator raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgnn_spmm.so")
+
+_lock = threading.Lock()
+_lib = None
+
+c_i32p = ctypes.c_void_p  # all device pointers travel as void*
+_VP = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
+_INT = ctypes.c_int
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "gnn_last_error": (ctypes.c_char_p, []),
+    "gnn_version": (ctypes.c_char_p, []),
+    "gnn_spmm_default_unit_nnz": (_I64, [_I64, _I64, _I64]),
+    "gnn_spmm_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
+    "gnn_spmm_csr_f32": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _SZ, _I64, _VP]),
+    "gnn_spmm_config": (_INT, [_I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_int32)]),
+    "gnn_spmm_set_timing_events": (None, [_VP, _VP]),
+    "gnn_segsort_workspace_bytes": (_SZ, [_I64]),
+    "gnn_build_operand_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "gnn_coo_to_csr": (_INT, [_VP, _VP, _I64, _I64, _VP, _VP, _VP]),
+    "gnn_csr_transpose_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
+    "gnn_csr_transpose": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "gnn_gather_rows_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
+}
+
+EXPORTED_SYMBOLS = tuple(_SIGNATURES)
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library. Raises if it is missing: no fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"gnn_amd: native library {LIB_PATH} is missing; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().gnn_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")

@@ -1,0 +1,942 @@
+// spmm.hip — MI355X (gfx950, CDNA4) kernels and C ABI of the SpMM aggregation path.
+//
+// What the reference does (spmm_cpp/cuda_spmm.cu:619-704): per call it converts the COO
+// indices to int32, zero-fills Y, builds a row pointer and a "virtual row" split of every
+// row into <=64-nnz chunks with a Blelloch scan (5-6 device syncs, 3 .item() reads, raw
+// cudaMalloc/cudaFree), then runs one 32-thread half-block per virtual row that gathers
+// X rows with scalar 4-byte loads and atomically adds each 64-column tile into Y.
+//
+// What this file does instead (design: DESIGN.md §Kernels):
+//  * The operand is CSR (int32 rowptr/col, fp32 val), built once per sampled layer by
+//    gnn_build_operand_f32 (the create_coo_tensor replacement) — no per-call conversion.
+//  * Load balance without a scan: the nonzeros are cut into fixed work units of S
+//    consecutive entries (S = unit_nnz). One 64-lane wave owns one unit; it finds its
+//    first/last row with a 64-way parallel search of rowptr and walks the rows in order.
+//    A row wholly inside a unit is stored straight to Y (empty rows store zeros, so Y is
+//    never memset); a row cut by a unit boundary stores its two partial sums to a slab,
+//    and a small second kernel adds the pieces in unit order. No atomics: results are
+//    deterministic.
+//  * Inside a wave, G lanes span the feature columns with VW-wide (8 or 16 byte) loads,
+//    NJ column chunks per lane, and the 64/G lane groups take different nonzeros of the
+//    same row; U nonzeros are issued back to back so U*NJ row loads are in flight per lane
+//    before the FMAs (memory-level parallelism for an HBM/Infinity-Cache bound gather).
+//  * Everything is stream-ordered on the caller's stream: no host syncs, no allocation.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "gnn_spmm.h"
+
+#ifndef GNN_BUILD_ID
+#define GNN_BUILD_ID "dev"
+#endif
+
+namespace {
+
+thread_local std::string g_err;
+thread_local hipEvent_t g_ev_start = nullptr;
+thread_local hipEvent_t g_ev_stop = nullptr;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define GNN_REQUIRE(cond, ...)                 \
+  do {                                         \
+    if (!(cond)) return fail(GNN_EINVAL, __VA_ARGS__); \
+  } while (0)
+
+#define GNN_LAUNCHED(name)                                                        \
+  do {                                                                            \
+    hipError_t e_ = hipGetLastError();                                            \
+    if (e_ != hipSuccess) return fail((int)e_, "%s launch: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+#define GNN_HIP(call, name)                                                       \
+  do {                                                                            \
+    hipError_t e_ = (call);                                                       \
+    if (e_ != hipSuccess) return fail((int)e_, "%s: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ---------------------------------------------------------------------------------
+// Vector types: clang ext vectors give global_load_dwordx2/x4 and per-lane packed FMA.
+// ---------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <int VW> struct Vec;
+template <> struct Vec<1> { using T = float; };
+template <> struct Vec<2> { using T = f2; };
+template <> struct Vec<4> { using T = f4; };
+
+template <int VW>
+__device__ __forceinline__ typename Vec<VW>::T vzero() { return typename Vec<VW>::T(0.0f); }
+
+// acc + v * x with one rounding per element (matches a C fmaf chain bit for bit).
+__device__ __forceinline__ float vfma(float v, float x, float acc) { return __builtin_fmaf(v, x, acc); }
+__device__ __forceinline__ f2 vfma(float v, f2 x, f2 acc) {
+  return f2{__builtin_fmaf(v, x.x, acc.x), __builtin_fmaf(v, x.y, acc.y)};
+}
+__device__ __forceinline__ f4 vfma(float v, f4 x, f4 acc) {
+  return f4{__builtin_fmaf(v, x.x, acc.x), __builtin_fmaf(v, x.y, acc.y),
+            __builtin_fmaf(v, x.z, acc.z), __builtin_fmaf(v, x.w, acc.w)};
+}
+
+__device__ __forceinline__ float shfl_xor_v(float x, int m) { return __shfl_xor(x, m); }
+__device__ __forceinline__ f2 shfl_xor_v(f2 x, int m) { return f2{__shfl_xor(x.x, m), __shfl_xor(x.y, m)}; }
+__device__ __forceinline__ f4 shfl_xor_v(f4 x, int m) {
+  return f4{__shfl_xor(x.x, m), __shfl_xor(x.y, m), __shfl_xor(x.z, m), __shfl_xor(x.w, m)};
+}
+
+__device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ float readlane_f(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+
+// Smallest r in [lo, hi) with pred(r) true (pred monotone false..true), hi if none.
+// 64 probes per round: ceil(log64(hi-lo)) dependent rounds (3 for 250k rows).
+template <class Pred>
+__device__ __forceinline__ int wave_first_true(int lo, int hi, int lane, Pred pred) {
+  while (lo < hi) {
+    const int n = hi - lo;
+    const int step = (n + 63) >> 6;
+    const int r = lo + lane * step;
+    const bool p = (r < hi) && pred(r);
+    const unsigned long long b = __ballot(p);
+    if (b == 0ull) {
+      lo = lo + ((n - 1) / step) * step + 1;
+    } else {
+      const int f = __builtin_ctzll(b);
+      hi = lo + f * step;
+      lo = (f == 0) ? hi : lo + (f - 1) * step + 1;
+    }
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------------------------
+// SpMM main kernel. One wave per work unit of S consecutive nonzeros.
+//   VW: floats per load (1/2/4); G: lanes per column group (64/32/16); NJ: column chunks
+//   per lane; U: nonzeros per lane group issued back to back.
+// Column of chunk j for a lane: tile_base + (lane % G) * VW + j * G * VW.
+// Slab layout: [nunits][2][ldslab]; slot 0 = piece of a row that began in an earlier unit,
+// slot 1 = piece of a row that begins in this unit and continues past it.
+// ---------------------------------------------------------------------------------
+template <int VW, int G, int NJ, int U>
+__global__ __launch_bounds__(256) void spmm_unit_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
+    int M, int nnz, int S, int nunits,
+    const float* __restrict__ X, int64_t ldx,
+    float* __restrict__ Y, int64_t ldy,
+    float* __restrict__ slab, int64_t ldslab, int F) {
+  using V = typename Vec<VW>::T;
+  constexpr int P = 64 / G;            // nonzeros taken side by side per step
+  constexpr int COVER = VW * G * NJ;   // columns covered by one column tile
+  const int lane = threadIdx.x & 63;
+  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nunits) return;  // wave-uniform; no block barriers below
+  const int sub = lane / G;
+  const int c0 = blockIdx.y * COVER + (lane % G) * VW;
+
+  const int ustart = u * S;  // host guarantees nunits * S fits in int
+  const int uend = min(ustart + S, nnz);
+  const bool last = (u == nunits - 1);
+
+  const int rlo = wave_first_true(0, M, lane, [&](int r) {
+    return rowptr[r + 1] > ustart || rowptr[r] >= ustart;
+  });
+  const int rhi = last ? M : wave_first_true(rlo, M, lane, [&](int r) { return rowptr[r] >= uend; });
+
+  for (int r = rlo; r < rhi; ++r) {
+    const int rb = rowptr[r];
+    const int re = rowptr[r + 1];
+    const int b = max(rb, ustart);
+    const int e = min(re, uend);
+    V acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = vzero<VW>();
+
+    for (int base = b; base < e; base += 64) {
+      const int n = min(64, e - base);
+      int mc = 0;
+      float mv = 0.0f;
+      if (lane < n) {
+        mc = col[base + lane];
+        mv = val[base + lane];
+      }
+      const int last_c = __shfl(mc, n - 1);
+      for (int k = 0; k < n; k += P * U) {
+        V xs[U][NJ];
+        float vs[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+          const int idx = k + t * P + sub;
+          int c;
+          float v;
+          if constexpr (P == 1) {
+            c = readlane_i(mc, idx);  // idx is wave-uniform: scalar row address
+            v = readlane_f(mv, idx);  // lanes >= n hold v = 0
+            if (idx >= n) c = last_c;  // padded slot re-reads a row already in flight
+          } else {
+            c = __shfl(mc, idx);
+            v = __shfl(mv, idx);
+            if (idx >= n) c = last_c;
+          }
+          vs[t] = v;
+          const float* xr = X + (int64_t)c * ldx;
+          // Columns past F load the row's last vector instead (same cache lines, no
+          // branch, no extra HBM bytes); those accumulator slots are never stored.
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int cc = min(c0 + j * G * VW, F - VW);
+            xs[t][j] = *reinterpret_cast<const V*>(xr + cc);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[j] = vfma(vs[t], xs[t][j], acc[j]);
+        }
+      }
+    }
+
+    if constexpr (P > 1) {
+#pragma unroll
+      for (int m = G; m < 64; m <<= 1) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] += shfl_xor_v(acc[j], m);
+      }
+    }
+
+    float* dst;
+    if (rb >= ustart && re <= uend) {
+      dst = Y + (int64_t)r * ldy;
+    } else {
+      dst = slab + ((int64_t)u * 2 + (rb < ustart ? 0 : 1)) * ldslab;
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cc = c0 + j * G * VW;
+      if ((j % P) == sub && cc < F) *reinterpret_cast<V*>(dst + cc) = acc[j];
+    }
+  }
+}
+
+// Adds the unit pieces of every row that straddles a unit boundary, in unit order.
+// Grid: (ceil(M/4), column chunks of 64*VW); one wave per (row, column chunk).
+template <int VW>
+__global__ __launch_bounds__(256) void spmm_combine_kernel(
+    const int* __restrict__ rowptr, int M, int S,
+    const float* __restrict__ slab, int64_t ldslab,
+    float* __restrict__ Y, int64_t ldy, int F) {
+  using V = typename Vec<VW>::T;
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const int rb = rowptr[r];
+  const int re = rowptr[r + 1];
+  if (re == rb) return;
+  const int u0 = rb / S;
+  const int u1 = (re - 1) / S;
+  if (u0 == u1) return;
+  const int cc = (blockIdx.y * 64 + lane) * VW;
+  if (cc >= F) return;
+  V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
+  int u = u0 + 1;
+  for (; u + 4 <= u1 + 1; u += 4) {
+    const V a0 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 0) * 2) * ldslab + cc);
+    const V a1 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 1) * 2) * ldslab + cc);
+    const V a2 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 2) * 2) * ldslab + cc);
+    const V a3 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 3) * 2) * ldslab + cc);
+    s += a0;
+    s += a1;
+    s += a2;
+    s += a3;
+  }
+  for (; u <= u1; ++u) s += *reinterpret_cast<const V*>(slab + ((int64_t)u * 2) * ldslab + cc);
+  *reinterpret_cast<V*>(Y + (int64_t)r * ldy + cc) = s;
+}
+
+// ---------------------------------------------------------------------------------
+// Operand builder: value = (float)((1.0 / full_degree(row)) * (double)normfact[col]),
+// the formula of cuda_spmm.cu:800 evaluated in double. One wave per row.
+// ---------------------------------------------------------------------------------
+template <typename CT>
+__global__ __launch_bounds__(256) void build_operand_kernel(
+    const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
+    const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
+    int* __restrict__ out_col, float* __restrict__ out_val) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int b = rowptr[r];
+  const int e = rowptr[r + 1];
+  if (b == e) return;
+  const double inv = 1.0 / (double)(fullrowptr[r + 1] - fullrowptr[r]);
+  for (int i = b + lane; i < e; i += 64) {
+    const int c = (int)colidx[i];
+    out_col[i] = c;
+    out_val[i] = (float)(inv * (double)normfact[c]);
+  }
+}
+
+// COO index image of a CSR: indices[0][i] = row(i), indices[1][i] = col[i].
+__global__ __launch_bounds__(256) void csr_to_coo_indices_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, int nrows, int64_t nnz,
+    int64_t* __restrict__ indices) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nrows) return;
+  const int b = rowptr[r];
+  const int e = rowptr[r + 1];
+  for (int i = b + lane; i < e; i += 64) {
+    indices[i] = r;
+    indices[nnz + i] = col[i];
+  }
+}
+
+// Sorted COO rows -> CSR row pointer by gap filling (thread i owns rows (row[i-1], row[i]]).
+__global__ __launch_bounds__(256) void coo_rowptr_kernel(const int64_t* __restrict__ row, int64_t nnz,
+                                                         int M, int* __restrict__ rowptr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i > nnz) return;
+  const int64_t prev = (i == 0) ? -1 : row[i - 1];
+  const int64_t cur = (i == nnz) ? (int64_t)M : row[i];
+  for (int64_t k = prev + 1; k <= cur; ++k) rowptr[k] = (int)i;
+}
+
+__global__ __launch_bounds__(256) void narrow_index_kernel(const int64_t* __restrict__ in, int64_t n,
+                                                           int* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (int)in[i];
+}
+
+// ---------------------------------------------------------------------------------
+// Exclusive scan of n int32 counts into out[0..n] (out[n] = total), one workgroup.
+// Optionally also writes the exclusive prefix into out2[0..n-1] (transpose cursors).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void scan_exclusive_kernel(const int* __restrict__ in, int n,
+                                                              int* __restrict__ out,
+                                                              int* __restrict__ out2) {
+  constexpr int ITEMS = 8;
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  int carry = 0;
+  for (int base = 0; base < n; base += 1024 * ITEMS) {
+    int v[ITEMS];
+    int tsum = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = base + tid * ITEMS + k;
+      v[k] = (idx < n) ? in[idx] : 0;
+      tsum += v[k];
+    }
+    int x = tsum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(x, d);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+      int w = (lane < 16) ? wsum[lane] : 0;
+#pragma unroll
+      for (int d = 1; d < 16; d <<= 1) {
+        const int y = __shfl_up(w, d);
+        if (lane >= d) w += y;
+      }
+      if (lane < 16) wsum[lane] = w;
+    }
+    __syncthreads();
+    int excl = carry + (wave ? wsum[wave - 1] : 0) + x - tsum;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+      const int idx = base + tid * ITEMS + k;
+      if (idx < n) {
+        out[idx] = excl;
+        if (out2) out2[idx] = excl;
+      }
+      excl += v[k];
+    }
+    carry += wsum[15];
+    __syncthreads();
+  }
+  if (tid == 0) out[n] = carry;
+}
+
+// ---------------------------------------------------------------------------------
+// Transpose helpers.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void col_count_kernel(const int* __restrict__ col, int64_t nnz,
+                                                        int* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < nnz) atomicAdd(&cnt[col[i]], 1);
+}
+
+// Wave per source row: each entry claims a slot in its column's output row. The slot
+// order inside an output row is arbitrary here; segsort restores ascending row order.
+__global__ __launch_bounds__(256) void transpose_scatter_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
+    int M, int* __restrict__ cursor, int* __restrict__ tr_col, float* __restrict__ tr_val) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const int b = rowptr[r];
+  const int e = rowptr[r + 1];
+  for (int i = b + lane; i < e; i += 64) {
+    const int pos = atomicAdd(&cursor[col[i]], 1);
+    tr_col[pos] = r;
+    tr_val[pos] = val[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Segmented sort, ascending by int32 key with an fp32 payload, in place.
+// Bitonic network in its "all comparators ascending" form (first step of every merge
+// compares mirrored positions), so positions >= L can be treated as +inf and skipped.
+// Segments: <=64 in registers, <=512 in a per-wave LDS region, <=16384 by one 1024-thread
+// workgroup in LDS, longer ones by one workgroup in global memory.
+// ---------------------------------------------------------------------------------
+constexpr int SEG_WAVE_LDS = 512;
+constexpr int SEG_BLOCK_LDS = 16384;
+
+__device__ __forceinline__ void cmpx_reg(int& k, float& v, int lane, int mask) {
+  const int pk = __shfl_xor(k, mask);
+  const float pv = __shfl_xor(v, mask);
+  const bool lower = lane < (lane ^ mask);
+  const bool take = lower ? (pk < k) : (pk > k);
+  if (take) {
+    k = pk;
+    v = pv;
+  }
+}
+
+// Pair p of a bitonic step -> element positions (i < j).
+__device__ __forceinline__ void bitonic_pair(int p, int size, int d, bool flip, int& i, int& j) {
+  if (flip) {
+    const int half = size >> 1;
+    i = (p / half) * size + (p % half);
+    j = i ^ (size - 1);
+  } else {
+    i = (p / d) * (2 * d) + (p % d);
+    j = i + d;
+  }
+}
+
+__global__ __launch_bounds__(256) void segsort_wave_kernel(const int* __restrict__ ptr, int nseg,
+                                                           int* __restrict__ key, float* __restrict__ val,
+                                                           int* __restrict__ counters,
+                                                           int* __restrict__ list_mid,
+                                                           int* __restrict__ list_long) {
+  __shared__ int sk[4][SEG_WAVE_LDS];
+  __shared__ float sv[4][SEG_WAVE_LDS];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int s = blockIdx.x * 4 + w;
+  if (s >= nseg) return;
+  const int b = ptr[s];
+  const int L = ptr[s + 1] - b;
+  if (L <= 1) return;
+  // already ascending?
+  bool bad = false;
+  for (int i = lane; i + 1 < L; i += 64) bad |= key[b + i] > key[b + i + 1];
+  if (__ballot(bad) == 0ull) return;
+
+  if (L <= 64) {
+    int k = (lane < L) ? key[b + lane] : INT_MAX;
+    float v = (lane < L) ? val[b + lane] : 0.0f;
+    for (int size = 2; size <= 64; size <<= 1) {
+      cmpx_reg(k, v, lane, size - 1);
+      for (int d = size >> 2; d >= 1; d >>= 1) cmpx_reg(k, v, lane, d);
+    }
+    if (lane < L) {
+      key[b + lane] = k;
+      val[b + lane] = v;
+    }
+    return;
+  }
+  if (L <= SEG_WAVE_LDS) {
+    int n = 1;
+    while (n < L) n <<= 1;
+    for (int i = lane; i < n; i += 64) {
+      sk[w][i] = (i < L) ? key[b + i] : INT_MAX;
+      sv[w][i] = (i < L) ? val[b + i] : 0.0f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int size = 2; size <= n; size <<= 1) {
+      for (int d = size >> 1; d >= 1; d >>= 1) {
+        const bool flip = (d == (size >> 1));
+        for (int p = lane; p < (n >> 1); p += 64) {
+          int i, j;
+          bitonic_pair(p, size, d, flip, i, j);
+          const int ki = sk[w][i], kj = sk[w][j];
+          if (kj < ki) {
+            const float vi = sv[w][i], vj = sv[w][j];
+            sk[w][i] = kj;
+            sk[w][j] = ki;
+            sv[w][i] = vj;
+            sv[w][j] = vi;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+    for (int i = lane; i < L; i += 64) {
+      key[b + i] = sk[w][i];
+      val[b + i] = sv[w][i];
+    }
+    return;
+  }
+  if (lane == 0) {
+    if (L <= SEG_BLOCK_LDS) {
+      list_mid[atomicAdd(&counters[0], 1)] = s;
+    } else {
+      list_long[atomicAdd(&counters[1], 1)] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void segsort_block_kernel(const int* __restrict__ ptr,
+                                                             int* __restrict__ key, float* __restrict__ val,
+                                                             const int* __restrict__ counters,
+                                                             const int* __restrict__ list) {
+  __shared__ int sk[SEG_BLOCK_LDS];
+  __shared__ float sv[SEG_BLOCK_LDS];
+  const int count = counters[0];
+  for (int t = blockIdx.x; t < count; t += gridDim.x) {
+    const int s = list[t];
+    const int b = ptr[s];
+    const int L = ptr[s + 1] - b;
+    int n = 1;
+    while (n < L) n <<= 1;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+      sk[i] = (i < L) ? key[b + i] : INT_MAX;
+      sv[i] = (i < L) ? val[b + i] : 0.0f;
+    }
+    __syncthreads();
+    for (int size = 2; size <= n; size <<= 1) {
+      for (int d = size >> 1; d >= 1; d >>= 1) {
+        const bool flip = (d == (size >> 1));
+        for (int p = threadIdx.x; p < (n >> 1); p += 1024) {
+          int i, j;
+          bitonic_pair(p, size, d, flip, i, j);
+          const int ki = sk[i], kj = sk[j];
+          if (kj < ki) {
+            const float vi = sv[i], vj = sv[j];
+            sk[i] = kj;
+            sk[j] = ki;
+            sv[i] = vj;
+            sv[j] = vi;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = threadIdx.x; i < L; i += 1024) {
+      key[b + i] = sk[i];
+      val[b + i] = sv[i];
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(1024) void segsort_global_kernel(const int* __restrict__ ptr,
+                                                              int* __restrict__ key, float* __restrict__ val,
+                                                              const int* __restrict__ counters,
+                                                              const int* __restrict__ list) {
+  const int count = counters[1];
+  for (int t = blockIdx.x; t < count; t += gridDim.x) {
+    const int s = list[t];
+    const int b = ptr[s];
+    const int L = ptr[s + 1] - b;
+    int64_t n = 1;
+    while (n < L) n <<= 1;
+    int* K = key + b;
+    float* Vv = val + b;
+    for (int64_t size = 2; size <= n; size <<= 1) {
+      for (int64_t d = size >> 1; d >= 1; d >>= 1) {
+        const bool flip = (d == (size >> 1));
+        for (int64_t p = threadIdx.x; p < (n >> 1); p += 1024) {
+          int64_t i, j;
+          if (flip) {
+            const int64_t half = size >> 1;
+            i = (p / half) * size + (p % half);
+            j = i ^ (size - 1);
+          } else {
+            i = (p / d) * (2 * d) + (p % d);
+            j = i + d;
+          }
+          if (j < L) {
+            const int ki = K[i], kj = K[j];
+            if (kj < ki) {
+              const float vi = Vv[i], vj = Vv[j];
+              K[i] = kj;
+              K[j] = ki;
+              Vv[i] = vj;
+              Vv[j] = vi;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Feature staging gather/scatter: one wave per row.
+// ---------------------------------------------------------------------------------
+template <int VW>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                          const int64_t* __restrict__ src_idx,
+                                                          float* __restrict__ dst, int64_t ld_dst,
+                                                          const int64_t* __restrict__ dst_idx,
+                                                          int64_t n, int F) {
+  using V = typename Vec<VW>::T;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int64_t s = src_idx ? src_idx[i] : i;
+  const int64_t d = dst_idx ? dst_idx[i] : i;
+  const float* sr = src + s * ld_src;
+  float* dr = dst + d * ld_dst;
+  for (int c = lane * VW; c < F; c += 64 * VW) {
+    *reinterpret_cast<V*>(dr + c) = *reinterpret_cast<const V*>(sr + c);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Host-side configuration and dispatch.
+// ---------------------------------------------------------------------------------
+struct SpmmCfg {
+  int vw, g, nj, tiles;
+  int64_t unit, nunits, ldslab;
+};
+
+int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
+  const uintptr_t px = (uintptr_t)X, py = (uintptr_t)Y;
+  if (F % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && px % 16 == 0 && py % 16 == 0) return 4;
+  if (F % 2 == 0 && ldx % 2 == 0 && ldy % 2 == 0 && px % 8 == 0 && py % 8 == 0) return 2;
+  return 1;
+}
+
+int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
+  (void)M;
+  (void)F;
+  // Aim for >= ~16k units (64 waves per CU) so the dispatcher can balance power-law
+  // rows; keep units >= 16 nonzeros so the per-unit search and the slab stay small.
+  int64_t s = ceil_div(nnz, 16384);
+  if (s < 16) s = 16;
+  if (s > 4096) s = 4096;
+  return s;
+}
+
+SpmmCfg make_cfg(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+                 const void* Y, int64_t unit) {
+  SpmmCfg c{};
+  c.vw = pick_vw(F, ldx, ldy, X, Y);
+  double best = -1.0;
+  const int gs[3] = {64, 32, 16};
+  for (int gi = 0; gi < 3; ++gi) {
+    const int g = gs[gi];
+    const int64_t lanecols = (int64_t)c.vw * g;
+    const int64_t tiles = ceil_div(F, lanecols * 8) > 0 ? ceil_div(F, lanecols * 8) : 1;
+    int64_t nj = ceil_div(F, lanecols * tiles);
+    if (nj < 1) nj = 1;
+    const double util = (double)F / (double)(tiles * lanecols * nj);
+    if (util > best + 1e-9) {
+      best = util;
+      c.g = g;
+      c.nj = (int)nj;
+      c.tiles = (int)tiles;
+    }
+  }
+  c.unit = unit > 0 ? unit : default_unit(M, nnz, F);
+  c.nunits = nnz > 0 ? ceil_div(nnz, c.unit) : 1;
+  c.ldslab = (int64_t)align_up((size_t)(F > 0 ? F : 1), 4);
+  return c;
+}
+
+using MainFn = void (*)(const int*, const int*, const float*, int, int, int, int, const float*, int64_t,
+                        float*, int64_t, float*, int64_t, int);
+
+constexpr int pick_u(int nj) { return nj <= 4 ? 4 : (nj == 5 ? 3 : 2); }
+
+template <int VW, int G, int NJ>
+MainFn main_ptr() {
+  return &spmm_unit_kernel<VW, G, NJ, pick_u(NJ)>;
+}
+
+template <int VW, int G>
+MainFn main_by_nj(int nj) {
+  switch (nj) {
+    case 1: return main_ptr<VW, G, 1>();
+    case 2: return main_ptr<VW, G, 2>();
+    case 3: return main_ptr<VW, G, 3>();
+    case 4: return main_ptr<VW, G, 4>();
+    case 5: return main_ptr<VW, G, 5>();
+    case 6: return main_ptr<VW, G, 6>();
+    case 7: return main_ptr<VW, G, 7>();
+    case 8: return main_ptr<VW, G, 8>();
+    default: return nullptr;
+  }
+}
+
+template <int VW>
+MainFn main_by_g(int g, int nj) {
+  switch (g) {
+    case 64: return main_by_nj<VW, 64>(nj);
+    case 32: return main_by_nj<VW, 32>(nj);
+    case 16: return main_by_nj<VW, 16>(nj);
+    default: return nullptr;
+  }
+}
+
+MainFn select_main(const SpmmCfg& c) {
+  switch (c.vw) {
+    case 4: return main_by_g<4>(c.g, c.nj);
+    case 2: return main_by_g<2>(c.g, c.nj);
+    case 1: return main_by_g<1>(c.g, c.nj);
+    default: return nullptr;
+  }
+}
+
+size_t segsort_ws(int64_t nseg) { return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * 4, 256) * 2; }
+
+int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hipStream_t st) {
+  if (nseg <= 0) return 0;
+  char* w = (char*)ws;
+  int* counters = (int*)w;
+  int* list_mid = (int*)(w + 256);
+  int* list_long = (int*)(w + 256 + align_up((size_t)nseg * 4, 256));
+  GNN_HIP(hipMemsetAsync(counters, 0, 16, st), "segsort counters memset");
+  segsort_wave_kernel<<<dim3((unsigned)ceil_div(nseg, 4)), dim3(256), 0, st>>>(ptr, (int)nseg, key, val, counters,
+                                                                            list_mid, list_long);
+  GNN_LAUNCHED("segsort_wave_kernel");
+  segsort_block_kernel<<<dim3(256), dim3(1024), 0, st>>>(ptr, key, val, counters, list_mid);
+  GNN_LAUNCHED("segsort_block_kernel");
+  segsort_global_kernel<<<dim3(16), dim3(1024), 0, st>>>(ptr, key, val, counters, list_long);
+  GNN_LAUNCHED("segsort_global_kernel");
+  return 0;
+}
+
+}  // namespace
+
+// =================================================================================
+// C ABI
+// =================================================================================
+extern "C" {
+
+const char* gnn_last_error(void) { return g_err.c_str(); }
+
+const char* gnn_version(void) { return "gnn_spmm gfx950 " GNN_BUILD_ID; }
+
+int64_t gnn_spmm_default_unit_nnz(int64_t M, int64_t nnz, int64_t F) { return default_unit(M, nnz, F); }
+
+size_t gnn_spmm_workspace_bytes(int64_t M, int64_t nnz, int64_t F, int64_t unit_nnz) {
+  const SpmmCfg c = make_cfg(M, nnz, F, F, F, nullptr, nullptr, unit_nnz);
+  return align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
+}
+
+int gnn_spmm_config(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y,
+                    int64_t unit_nnz, int32_t out[6]) {
+  GNN_REQUIRE(out != nullptr, "gnn_spmm_config: out is NULL");
+  const SpmmCfg c = make_cfg(M, nnz, F, ldx, ldy, X, Y, unit_nnz);
+  out[0] = c.vw;
+  out[1] = c.g;
+  out[2] = c.nj;
+  out[3] = c.tiles;
+  out[4] = (int32_t)c.unit;
+  out[5] = (int32_t)c.nunits;
+  return 0;
+}
+
+void gnn_spmm_set_timing_events(void* start, void* stop) {
+  g_ev_start = (hipEvent_t)start;
+  g_ev_stop = (hipEvent_t)stop;
+}
+
+int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t M, int64_t K,
+                     int64_t nnz, const float* X, int64_t ldx, float* Y, int64_t ldy, int64_t F,
+                     void* workspace, size_t workspace_bytes, int64_t unit_nnz, void* stream) {
+  hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
+  g_ev_start = g_ev_stop = nullptr;
+  GNN_REQUIRE(M >= 0 && K >= 0 && nnz >= 0 && F >= 0, "gnn_spmm_csr_f32: negative size");
+  GNN_REQUIRE(M < INT_MAX && K < INT_MAX && nnz < INT_MAX, "gnn_spmm_csr_f32: M, K, nnz must be < 2^31");
+  GNN_REQUIRE(F <= ldx || K == 0, "gnn_spmm_csr_f32: F (%lld) > ldx (%lld)", (long long)F, (long long)ldx);
+  GNN_REQUIRE(F <= ldy || M == 0, "gnn_spmm_csr_f32: F (%lld) > ldy (%lld)", (long long)F, (long long)ldy);
+  if (M == 0 || F == 0) return 0;
+  GNN_REQUIRE(rowptr && Y, "gnn_spmm_csr_f32: NULL rowptr/Y");
+  GNN_REQUIRE(nnz == 0 || (col && val && X), "gnn_spmm_csr_f32: NULL col/val/X");
+  const SpmmCfg c = make_cfg(M, nnz, F, ldx, ldy, X, Y, unit_nnz);
+  GNN_REQUIRE(c.nunits * c.unit < (int64_t)INT_MAX + c.unit, "gnn_spmm_csr_f32: unit overflow");
+  GNN_REQUIRE(c.nunits <= (int64_t)INT_MAX / 2, "gnn_spmm_csr_f32: too many units");
+  const size_t need = align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
+  const bool any_split = c.nunits > 1;
+  GNN_REQUIRE(!any_split || (workspace && workspace_bytes >= need),
+              "gnn_spmm_csr_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
+  GNN_REQUIRE((uintptr_t)workspace % 16 == 0, "gnn_spmm_csr_f32: workspace not 16-byte aligned");
+  MainFn fn = select_main(c);
+  GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no kernel for vw=%d g=%d nj=%d", c.vw, c.g, c.nj);
+  hipStream_t st = (hipStream_t)stream;
+  float* slab = (float*)workspace;
+  const dim3 grid((unsigned)ceil_div(c.nunits, 4), (unsigned)c.tiles);
+  if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
+  hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
+                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F);
+  GNN_LAUNCHED("spmm_unit_kernel");
+  if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
+  if (any_split) {
+    const dim3 g2((unsigned)ceil_div(M, 4), (unsigned)ceil_div(F, 64 * c.vw));
+    switch (c.vw) {
+      case 4:
+        spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        break;
+      case 2:
+        spmm_combine_kernel<2><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        break;
+      default:
+        spmm_combine_kernel<1><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        break;
+    }
+    GNN_LAUNCHED("spmm_combine_kernel");
+  }
+  return 0;
+}
+
+size_t gnn_segsort_workspace_bytes(int64_t nseg) { return segsort_ws(nseg); }
+
+int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
+                          const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col,
+                          float* csr_val, int64_t* coo_indices, void* workspace, size_t workspace_bytes,
+                          void* stream) {
+  GNN_REQUIRE(nrows >= 0 && ncols >= 0 && nnz >= 0, "gnn_build_operand_f32: negative size");
+  GNN_REQUIRE(nrows < INT_MAX && ncols < INT_MAX && nnz < INT_MAX, "gnn_build_operand_f32: sizes must be < 2^31");
+  GNN_REQUIRE(colidx_bytes == 2 || colidx_bytes == 4 || colidx_bytes == 8,
+              "gnn_build_operand_f32: colidx_bytes must be 2, 4 or 8 (got %d)", colidx_bytes);
+  if (nrows == 0 || nnz == 0) return 0;
+  GNN_REQUIRE(fullrowptr && rowptr && colidx && normfact && csr_col && csr_val, "gnn_build_operand_f32: NULL input");
+  GNN_REQUIRE(workspace && workspace_bytes >= segsort_ws(nrows), "gnn_build_operand_f32: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)ceil_div(nrows, 4));
+  switch (colidx_bytes) {
+    case 2:
+      build_operand_kernel<int16_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val);
+      break;
+    case 4:
+      build_operand_kernel<int32_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val);
+      break;
+    default:
+      build_operand_kernel<int64_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val);
+      break;
+  }
+  GNN_LAUNCHED("build_operand_kernel");
+  int rc = run_segsort(rowptr, nrows, csr_col, csr_val, workspace, st);
+  if (rc) return rc;
+  if (coo_indices) {
+    csr_to_coo_indices_kernel<<<grid, dim3(256), 0, st>>>(rowptr, csr_col, (int)nrows, nnz, coo_indices);
+    GNN_LAUNCHED("csr_to_coo_indices_kernel");
+  }
+  return 0;
+}
+
+int gnn_coo_to_csr(const int64_t* row, const int64_t* col, int64_t nnz, int64_t M, int32_t* rowptr, int32_t* col32,
+                   void* stream) {
+  GNN_REQUIRE(nnz >= 0 && M >= 0, "gnn_coo_to_csr: negative size");
+  GNN_REQUIRE(nnz < INT_MAX && M < INT_MAX, "gnn_coo_to_csr: sizes must be < 2^31");
+  GNN_REQUIRE(rowptr != nullptr, "gnn_coo_to_csr: NULL rowptr");
+  GNN_REQUIRE(nnz == 0 || row != nullptr, "gnn_coo_to_csr: NULL row");
+  hipStream_t st = (hipStream_t)stream;
+  coo_rowptr_kernel<<<dim3((unsigned)ceil_div(nnz + 1, 256)), dim3(256), 0, st>>>(row, nnz, (int)M, rowptr);
+  GNN_LAUNCHED("coo_rowptr_kernel");
+  if (col32 && nnz > 0) {
+    GNN_REQUIRE(col != nullptr, "gnn_coo_to_csr: NULL col");
+    narrow_index_kernel<<<dim3((unsigned)ceil_div(nnz, 256)), dim3(256), 0, st>>>(col, nnz, col32);
+    GNN_LAUNCHED("narrow_index_kernel");
+  }
+  return 0;
+}
+
+size_t gnn_csr_transpose_workspace_bytes(int64_t M, int64_t K, int64_t nnz) {
+  (void)M;
+  (void)nnz;
+  return align_up((size_t)(K > 0 ? K : 1) * 4, 256) + segsort_ws(K);
+}
+
+int gnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val, int64_t M, int64_t K, int64_t nnz,
+                      int32_t* tr_rowptr, int32_t* tr_col, float* tr_val, void* workspace, size_t workspace_bytes,
+                      void* stream) {
+  GNN_REQUIRE(M >= 0 && K >= 0 && nnz >= 0, "gnn_csr_transpose: negative size");
+  GNN_REQUIRE(M < INT_MAX && K < INT_MAX && nnz < INT_MAX, "gnn_csr_transpose: sizes must be < 2^31");
+  GNN_REQUIRE(tr_rowptr != nullptr, "gnn_csr_transpose: NULL tr_rowptr");
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 0) return 0;
+  if (nnz == 0 || M == 0) {
+    GNN_HIP(hipMemsetAsync(tr_rowptr, 0, (size_t)(K + 1) * 4, st), "transpose memset");
+    return 0;
+  }
+  GNN_REQUIRE(rowptr && col && val && tr_col && tr_val, "gnn_csr_transpose: NULL input/output");
+  GNN_REQUIRE(workspace && workspace_bytes >= gnn_csr_transpose_workspace_bytes(M, K, nnz),
+              "gnn_csr_transpose: workspace too small");
+  char* w = (char*)workspace;
+  int* cnt = (int*)w;
+  void* ssws = w + align_up((size_t)K * 4, 256);
+  GNN_HIP(hipMemsetAsync(cnt, 0, (size_t)K * 4, st), "transpose count memset");
+  col_count_kernel<<<dim3((unsigned)ceil_div(nnz, 256)), dim3(256), 0, st>>>(col, nnz, cnt);
+  GNN_LAUNCHED("col_count_kernel");
+  scan_exclusive_kernel<<<dim3(1), dim3(1024), 0, st>>>(cnt, (int)K, tr_rowptr, cnt);
+  GNN_LAUNCHED("scan_exclusive_kernel");
+  transpose_scatter_kernel<<<dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, st>>>(rowptr, col, val, (int)M, cnt,
+                                                                               tr_col, tr_val);
+  GNN_LAUNCHED("transpose_scatter_kernel");
+  return run_segsort(tr_rowptr, K, tr_col, tr_val, ssws, st);
+}
+
+int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx, float* dst, int64_t ld_dst,
+                        const int64_t* dst_idx, int64_t n, int64_t F, void* stream) {
+  GNN_REQUIRE(n >= 0 && F >= 0, "gnn_gather_rows_f32: negative size");
+  GNN_REQUIRE(F <= ld_src && F <= ld_dst, "gnn_gather_rows_f32: F exceeds a row stride");
+  GNN_REQUIRE(F < INT_MAX, "gnn_gather_rows_f32: F too large");
+  if (n == 0 || F == 0) return 0;
+  GNN_REQUIRE(src && dst, "gnn_gather_rows_f32: NULL src/dst");
+  hipStream_t st = (hipStream_t)stream;
+  const int vw = pick_vw(F, ld_src, ld_dst, src, dst);
+  const dim3 grid((unsigned)ceil_div(n, 4));
+  switch (vw) {
+    case 4:
+      gather_rows_kernel<4><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+    case 2:
+      gather_rows_kernel<2><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+    default:
+      gather_rows_kernel<1><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+  }
+  GNN_LAUNCHED("gather_rows_kernel");
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,302 @@
+"""Sparse x dense aggregation operator — drop-in for the reference's ``custom_sparse_ops``.
+
+Reference interface (custom_sparse_ops.py:1-43, spmm_cpp/spmm.cpp:1-56):
+  * ``spmm = SparseDenseMM.apply`` — Y = A·X for a coalesced sparse COO ``A`` (M x K) on
+    the GPU and a dense fp32 ``X`` (K x F); backward returns ``(None, Aᵀ·G)``
+    (custom_sparse_ops.py:16-37). No gradient flows to the sparse values.
+  * ``create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols)`` — the
+    sampled-adjacency builder (spmm.cpp:44-50, cuda_spmm.cu:787-827).
+  * module floats ``spmm_forward_time`` / ``spmm_backward_time`` read by main.py:196.
+  * native entry points ``spmm_load_balance`` / ``spmm_naive`` (spmm.cpp:23-42).
+
+Here every call lands in libgnn_spmm.so (HIP, gfx950) through its C ABI, stream-ordered on
+torch's current stream with no host synchronisation. The CSR image of an operand is built
+once (by ``create_coo_tensor`` or on first use of a foreign COO tensor) and cached on the
+tensor; the transpose needed by backward is built on the GPU once and cached too, instead
+of the reference's per-backward ``A.transpose(0,1).coalesce()`` sort.
+
+Error behaviour mirrors the reference's TORCH_CHECKs (spmm.cpp:10-21): RuntimeError
+"<arg> must be a CUDA tensor" / "must be coalesced" / "must be contiguous". There is no CPU
+path: CPU tensors raise, as the reference's do.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+# Reference module-level timers (custom_sparse_ops.py:11-12). Accumulated in seconds from
+# HIP events when timing is enabled (enable_timing(True)); 0.0 otherwise, as upstream.
+spmm_forward_time = 0.0
+spmm_backward_time = 0.0
+
+_timing_enabled = False
+_timing_records: List[Tuple[str, "torch.cuda.Event", "torch.cuda.Event", int]] = []
+
+
+def enable_timing(flag: bool = True) -> None:
+    """Record HIP events around every aggregation kernel (main kernel only)."""
+    global _timing_enabled
+    _timing_enabled = bool(flag)
+
+
+def take_timing_records(sync: bool = True):
+    """Return [(tag, ms, algorithmic_bytes)] for recorded calls and clear the list.
+
+    Also folds the times into spmm_forward_time / spmm_backward_time (seconds)."""
+    global spmm_forward_time, spmm_backward_time
+    if sync and _timing_records:
+        _timing_records[-1][2].synchronize()
+    out = []
+    for tag, e0, e1, nbytes in _timing_records:
+        ms = e0.elapsed_time(e1)
+        out.append((tag, ms, nbytes))
+        if tag.startswith("fwd"):
+            spmm_forward_time += ms * 1e-3
+        else:
+            spmm_backward_time += ms * 1e-3
+    _timing_records.clear()
+    return out
+
+
+def algorithmic_bytes(M: int, nnz: int, F: int) -> int:
+    """gathered X rows + (col, val) + rowptr + Y write."""
+    return nnz * F * 4 + nnz * 8 + (M + 1) * 4 + M * F * 4
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _require(cond: bool, msg: str) -> None:
+    if not cond:
+        raise RuntimeError(msg)
+
+
+class CsrOperand:
+    """Device CSR image of a sampled adjacency A (M x K).
+
+    rowptr int32[M+1], col int32[nnz], val fp32[nnz], columns ascending inside each row.
+    ``transpose()`` returns (and caches) the canonical CSR of Aᵀ (K x M)."""
+
+    __slots__ = ("rowptr", "col", "val", "shape", "nnz", "_t", "__weakref__")
+
+    def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, shape: Tuple[int, int]):
+        self.rowptr = rowptr
+        self.col = col
+        self.val = val
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.nnz = int(col.numel())
+        self._t: Optional["CsrOperand"] = None
+
+    @property
+    def device(self) -> torch.device:
+        return self.val.device
+
+    def transpose(self) -> "CsrOperand":
+        if self._t is None:
+            M, K = self.shape
+            dev = self.device
+            with torch.cuda.device(dev):
+                L = _lib.lib()
+                tr_rowptr = torch.empty(K + 1, dtype=torch.int32, device=dev)
+                tr_col = torch.empty(self.nnz, dtype=torch.int32, device=dev)
+                tr_val = torch.empty(self.nnz, dtype=torch.float32, device=dev)
+                wsb = L.gnn_csr_transpose_workspace_bytes(M, K, self.nnz)
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                _lib.check(L.gnn_csr_transpose(_ptr(self.rowptr), _ptr(self.col), _ptr(self.val), M, K, self.nnz,
+                                               _ptr(tr_rowptr), _ptr(tr_col), _ptr(tr_val), _ptr(ws), wsb,
+                                               _stream(dev)), "gnn_csr_transpose")
+            t = CsrOperand(tr_rowptr, tr_col, tr_val, (K, M))
+            t._t = self
+            self._t = t
+        return self._t
+
+    def to_torch_coo(self) -> torch.Tensor:
+        """Coalesced torch COO view of the operand (int64 indices, shared values)."""
+        M, _ = self.shape
+        rows = torch.repeat_interleave(torch.arange(M, device=self.device),
+                                       (self.rowptr[1:] - self.rowptr[:-1]).long())
+        idx = torch.stack([rows, self.col.long()])
+        return torch.sparse_coo_tensor(idx, self.val, self.shape, is_coalesced=True)
+
+
+def csr_of(mat: "torch.Tensor | CsrOperand") -> CsrOperand:
+    """CSR image of a sampled operand: cached one, or built on the GPU from a coalesced COO."""
+    if isinstance(mat, CsrOperand):
+        return mat
+    plan = getattr(mat, "_gnn_csr", None)
+    if plan is not None:
+        return plan
+    _require(isinstance(mat, torch.Tensor) and mat.is_sparse, "sparseMat must be a sparse COO tensor")
+    _require(mat.is_cuda, "sparseMat must be a CUDA tensor")
+    _require(mat.is_coalesced(), "sparseMat must be coalesced")
+    _require(mat.dtype == torch.float32, "sparseMat must be float32")
+    M, K = mat.shape
+    nnz = mat._nnz()
+    _require(M < 2**31 and K < 2**31 and nnz < 2**31, "sparseMat dims and nnz must be < 2^31")
+    dev = mat.device
+    idx = mat._indices()
+    with torch.cuda.device(dev):
+        rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(nnz, dtype=torch.int32, device=dev)
+        L = _lib.lib()
+        row_ptr = idx[0].data_ptr() if nnz else None
+        col_ptr = idx[1].data_ptr() if nnz else None
+        if nnz and not idx.is_contiguous():
+            idx = idx.contiguous()
+            row_ptr, col_ptr = idx[0].data_ptr(), idx[1].data_ptr()
+        _lib.check(L.gnn_coo_to_csr(row_ptr, col_ptr, nnz, M, _ptr(rowptr), _ptr(col) if nnz else None,
+                                    _stream(dev)), "gnn_coo_to_csr")
+    plan = CsrOperand(rowptr, col, mat._values().contiguous(), (M, K))
+    try:
+        mat._gnn_csr = plan
+    except AttributeError:  # pragma: no cover - tensors normally accept attributes
+        pass
+    return plan
+
+
+def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: int = 0) -> torch.Tensor:
+    """Y = A·X on the GPU. ``dense`` must be fp32, row-major rows (stride(1) == 1); a padded
+    row stride (stride(0) > F) is accepted and read in place."""
+    _require(dense.is_cuda, "denseMat must be a CUDA tensor")
+    _require(dense.dim() == 2, "denseMat must be 2-D")
+    _require(dense.dtype == torch.float32, "denseMat must be float32")
+    _require(dense.stride(1) == 1 or dense.shape[1] <= 1, "denseMat must be contiguous")
+    M, K = op.shape
+    _require(dense.shape[0] == K, f"size mismatch: sparse {tuple(op.shape)} @ dense {tuple(dense.shape)}")
+    _require(dense.device == op.device, "sparseMat and denseMat must be on the same device")
+    F = dense.shape[1]
+    ldx = dense.stride(0) if dense.shape[0] > 1 else max(F, 1)
+    dev = dense.device
+    with torch.cuda.device(dev):
+        out = torch.empty((M, F), dtype=torch.float32, device=dev)
+        if M == 0 or F == 0:
+            return out
+        L = _lib.lib()
+        wsb = L.gnn_spmm_workspace_bytes(M, op.nnz, F, unit_nnz)
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        st = _stream(dev)
+        if _timing_enabled:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()  # creates the underlying hipEvent; the library re-records it
+            e1.record()
+            L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
+            _timing_records.append((tag, e0, e1, algorithmic_bytes(M, op.nnz, F)))
+        _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
+                                      dense.data_ptr(), ldx, out.data_ptr(), F, F,
+                                      ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32")
+    return out
+
+
+class SparseDenseMM(torch.autograd.Function):
+    """custom_sparse_ops.py:16-37: forward A·X, backward (None, Aᵀ·G)."""
+
+    @staticmethod
+    def forward(ctx, mat1, mat2):
+        op = csr_of(mat1)
+        _require(mat2.is_cuda, "denseMat must be a CUDA tensor")
+        ctx.op = op
+        return spmm_csr(op, mat2, tag="fwd")
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        op_t = ctx.op.transpose()
+        return None, spmm_csr(op_t, grad_output.contiguous(), tag="bwd")
+
+
+spmm = SparseDenseMM.apply
+
+
+def spmm_load_balance(sparseMat, denseMat) -> torch.Tensor:
+    """Native entry point of spmm.cpp:23-27 (no autograd)."""
+    _require(isinstance(sparseMat, CsrOperand) or sparseMat.is_cuda, "sparseMat must be a CUDA tensor")
+    if isinstance(sparseMat, torch.Tensor):
+        _require(sparseMat.is_coalesced(), "sparseMat must be coalesced")
+    _require(denseMat.is_cuda, "denseMat must be a CUDA tensor")
+    _require(denseMat.is_contiguous(), "denseMat must be contiguous")
+    return spmm_csr(csr_of(sparseMat), denseMat)
+
+
+# spmm.cpp:38-42 binds a second kernel with the same math; one kernel serves both here.
+spmm_naive = spmm_load_balance
+
+
+def _seg_ws(nrows: int, dev) -> Tuple[torch.Tensor, int]:
+    wsb = _lib.lib().gnn_segsort_workspace_bytes(nrows)
+    return torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev), wsb
+
+
+def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.Tensor, normfact: torch.Tensor,
+                  nrows: int, ncols: int, with_coo: bool = True):
+    """Device operand from the sampler's CSR pieces. Returns (CsrOperand, coo_indices|None)."""
+    for name, t in (("fullrowptr", fullrowptr), ("rowptr", rowptr), ("normfact", normfact)):
+        _require(t.is_cuda, f"{name} must be a CUDA tensor")
+        _require(t.is_contiguous(), f"{name} must be contiguous")
+    _require(colidx.is_cuda, "colidx must be a CUDA tensor")
+    _require(fullrowptr.dtype == torch.int32 and rowptr.dtype == torch.int32, "row pointers must be int32")
+    _require(normfact.dtype == torch.float32, "normfact must be float32")
+    _require(colidx.dtype in (torch.int16, torch.int32, torch.int64), "colidx must be int16/int32/int64")
+    _require(rowptr.numel() == nrows + 1 and fullrowptr.numel() == nrows + 1, "row pointer length != nrows + 1")
+    colidx = colidx.contiguous()
+    nnz = colidx.numel()
+    dev = colidx.device
+    with torch.cuda.device(dev):
+        col32 = torch.empty(nnz, dtype=torch.int32, device=dev)
+        val = torch.empty(nnz, dtype=torch.float32, device=dev)
+        coo = torch.empty((2, nnz), dtype=torch.int64, device=dev) if with_coo else None
+        ws, wsb = _seg_ws(nrows, dev)
+        _lib.check(_lib.lib().gnn_build_operand_f32(
+            _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
+            nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _ptr(ws), wsb, _stream(dev)),
+            "gnn_build_operand_f32")
+    return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
+
+
+def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> torch.Tensor:
+    """spmm.cpp:44-50 / cuda_spmm.cu:806-827: coalesced sparse COO of the sampled layer with
+    value = (1/full_degree(row)) * normfact[col] (double math, fp32 store). The CSR image
+    is cached on the returned tensor for the aggregation kernels."""
+    op, coo = build_operand(fullrowptr, rowptr, colidx, normfact, int(nrows), int(ncols), with_coo=True)
+    t = torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols)), is_coalesced=True)
+    t._gnn_csr = op
+    return t
+
+
+def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.Tensor,
+                dst_idx: Optional[torch.Tensor], n: Optional[int] = None) -> None:
+    """dst[dst_idx] = src[src_idx] row copy on the GPU (int64 indices, fp32 rows)."""
+    _require(src.is_cuda and dst.is_cuda, "gather_rows tensors must be CUDA tensors")
+    _require(src.dtype == torch.float32 and dst.dtype == torch.float32, "gather_rows tensors must be float32")
+    _require(src.stride(1) == 1 and dst.stride(1) == 1, "gather_rows rows must be contiguous")
+    F = dst.shape[1]
+    _require(src.shape[1] >= F, "gather_rows: source rows narrower than destination")
+    if n is None:
+        n = int((src_idx if src_idx is not None else dst_idx).numel()) if (src_idx is not None or dst_idx is not None) \
+            else int(src.shape[0])
+    for t in (src_idx, dst_idx):
+        if t is not None:
+            _require(t.is_cuda and t.dtype == torch.int64 and t.is_contiguous(), "gather_rows indices must be int64 CUDA")
+    dev = dst.device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().gnn_gather_rows_f32(src.data_ptr(), src.stride(0), _ptr(src_idx), dst.data_ptr(),
+                                                  dst.stride(0), _ptr(dst_idx), n, F, _stream(dev)),
+                   "gnn_gather_rows_f32")
+
+
+def spmm_config(M: int, nnz: int, F: int, ldx: Optional[int] = None, ldy: Optional[int] = None,
+                unit_nnz: int = 0) -> dict:
+    """Kernel configuration the library picks for a call shape (16-byte aligned buffers)."""
+    out = (ctypes.c_int32 * 6)()
+    _lib.check(_lib.lib().gnn_spmm_config(M, nnz, F, ldx or F, ldy or F, 256, 256, unit_nnz, out), "gnn_spmm_config")
+    return dict(vw=out[0], g=out[1], nj=out[2], tiles=out[3], unit_nnz=out[4], units=out[5])

@@ -1,0 +1,128 @@
+/*
+ * gnn_spmm.h — C ABI of the MI355X-native SpMM-aggregation path (libgnn_spmm.so).
+ *
+ * This is the drop-in boundary for the reference's CUDA extension `spmm`
+ * (reference: spmm_cpp/spmm.cpp:52-56, bound in custom_sparse_ops.py:8). Every entry
+ * point takes plain device pointers, sizes and a hipStream_t (passed as void*), launches
+ * stream-ordered work only (no host synchronisation, no allocation, graph-capturable),
+ * and returns 0 on success or a non-zero status whose text is gnn_last_error().
+ *
+ * Status codes: 0 = ok; GNN_EINVAL (-22) = bad argument (shape, alignment, workspace);
+ * any positive value = the hipError_t of a failed launch.
+ *
+ * Index types: CSR row pointers and column indices are int32 (the reference narrows its
+ * int64 COO indices to int32 too: cuda_spmm.cu:620-621), so M, K and nnz must be < 2^31.
+ */
+#ifndef GNN_SPMM_H
+#define GNN_SPMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNN_EINVAL (-22)
+
+/* Text of the last error raised on the calling thread ("" if none). */
+const char* gnn_last_error(void);
+
+/* Library version string (build id). */
+const char* gnn_version(void);
+
+/* ---------------------------------------------------------------------------------
+ * SpMM forward / backward:  Y[M, F] = A[M, K] · X[K, F]   (fp32, CSR operand)
+ *
+ * Replaces: spmm_load_balance(sparseMat, denseMat)   spmm_cpp/spmm.cpp:23-27
+ *           -> spmm_cuda_v2                           spmm_cpp/cuda_spmm.cu:619-704
+ *           and spmm_naive (spmm.cpp:38-42, same math, no load balance).
+ * The reference's backward is the same call on A^T (custom_sparse_ops.py:33-37); here the
+ * caller passes the CSR of A^T produced by gnn_csr_transpose.
+ *
+ * X rows are read with stride ldx (elements), Y rows written with stride ldy; F <= ldx,
+ * F <= ldy. Every one of the M rows of Y (columns [0, F)) is written (empty rows get 0),
+ * so Y needs no zero-fill. Rows are summed in CSR order inside a work unit of `unit_nnz`
+ * nonzeros; rows that straddle units are combined in unit order by a second kernel, so the
+ * result is deterministic (bitwise reproducible run to run).
+ *
+ * `workspace` must hold gnn_spmm_workspace_bytes(M, nnz, F, unit_nnz) bytes (device
+ * memory); unit_nnz <= 0 selects gnn_spmm_default_unit_nnz(M, nnz, F).
+ * ------------------------------------------------------------------------------- */
+int64_t gnn_spmm_default_unit_nnz(int64_t M, int64_t nnz, int64_t F);
+size_t gnn_spmm_workspace_bytes(int64_t M, int64_t nnz, int64_t F, int64_t unit_nnz);
+int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val,
+                     int64_t M, int64_t K, int64_t nnz,
+                     const float* X, int64_t ldx,
+                     float* Y, int64_t ldy, int64_t F,
+                     void* workspace, size_t workspace_bytes, int64_t unit_nnz,
+                     void* stream);
+
+/* Describe the kernel configuration gnn_spmm_csr_f32 would pick (vector width, lanes per
+ * column group, column chunks per lane, column tiles, units). For diagnostics/benchmarks. */
+int gnn_spmm_config(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,
+                    const void* X, const void* Y, int64_t unit_nnz, int32_t out[6]);
+
+/* Optional timing hook: when set, the NEXT gnn_spmm_csr_f32 call on this thread records
+ * `start` immediately before and `stop` immediately after its main aggregation kernel on
+ * the call's stream, then clears the hook. Events are hipEvent_t passed as void*. */
+void gnn_spmm_set_timing_events(void* start, void* stop);
+
+/* ---------------------------------------------------------------------------------
+ * Sampled-adjacency operand builder.
+ *
+ * Replaces: create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols)
+ *           spmm_cpp/spmm.cpp:44-50 -> to_coo_tensor / _create_coo_tensor_kernel
+ *           spmm_cpp/cuda_spmm.cu:787-827 (called from sampler.py:135-139).
+ * For row r and each entry i in [rowptr[r], rowptr[r+1]):
+ *     val[i] = (float)((1.0 / (double)(fullrowptr[r+1] - fullrowptr[r])) * (double)normfact[col[i]])
+ * (double arithmetic, single rounding to fp32, as cuda_spmm.cu:800).
+ * colidx may be int16 (colidx_bytes = 2, sign-extended like the reference's int16
+ * accessor), int32 (4) or int64 (8). Rows whose columns are not ascending are sorted
+ * (key = column, payload = value), which is what the reference's .coalesce() does
+ * (cuda_spmm.cu:825); rows are assumed free of duplicate columns (scipy slicing output).
+ * Outputs: csr_col (int32, nnz), csr_val (fp32, nnz) and, if coo_indices != NULL, the
+ * coalesced COO indices int64[2][nnz] (row-major: all rows then all columns).
+ * `workspace` >= gnn_segsort_workspace_bytes(nrows) bytes.
+ * ------------------------------------------------------------------------------- */
+size_t gnn_segsort_workspace_bytes(int64_t nseg);
+int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr,
+                          const void* colidx, int colidx_bytes,
+                          const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz,
+                          int32_t* csr_col, float* csr_val, int64_t* coo_indices,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Format conversions (replace the per-call preprocessing of cuda_spmm.cu:620-667 and the
+ * backward's A.transpose(0,1).coalesce() of custom_sparse_ops.py:34).
+ * ------------------------------------------------------------------------------- */
+
+/* Coalesced COO (int64 row and column index arrays, rows ascending) -> CSR row pointer
+ * (int32, M+1) and int32 column indices. `col32` may be NULL to skip the narrowing. */
+int gnn_coo_to_csr(const int64_t* row, const int64_t* col, int64_t nnz, int64_t M,
+                   int32_t* rowptr, int32_t* col32, void* stream);
+
+/* CSR (M x K) -> CSR of the transpose (K x M), canonical: rows ascending inside every
+ * output row, i.e. identical to A.t().coalesce(). Deterministic.
+ * tr_rowptr: int32[K+1], tr_col: int32[nnz], tr_val: fp32[nnz].
+ * `workspace` >= gnn_csr_transpose_workspace_bytes(M, K, nnz). */
+size_t gnn_csr_transpose_workspace_bytes(int64_t M, int64_t K, int64_t nnz);
+int gnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val,
+                      int64_t M, int64_t K, int64_t nnz,
+                      int32_t* tr_rowptr, int32_t* tr_col, float* tr_val,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Feature staging (replaces the masked gathers of main.py:129-134).
+ * dst[dst_idx[i], 0:F] = src[src_idx[i], 0:F] for i in [0, n). A NULL src_idx / dst_idx
+ * means the identity. Row strides in elements. Indices int64.
+ * ------------------------------------------------------------------------------- */
+int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx,
+                        float* dst, int64_t ld_dst, const int64_t* dst_idx,
+                        int64_t n, int64_t F, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNN_SPMM_H */

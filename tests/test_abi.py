@@ -1,0 +1,83 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/gnn_spmm.h declares;
+host-side configuration logic (no kernel launches — there is no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from gnn_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    with open(os.path.join(REPO, "include", "gnn_spmm.h")) as f:
+        txt = f.read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gnn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    L = _lib.lib()
+    decl = _declared()
+    assert len(decl) >= 12
+    for name in decl:
+        assert hasattr(L, name), f"{name} declared in gnn_spmm.h but not exported"
+    assert set(decl) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_version_and_error_strings():
+    L = _lib.lib()
+    assert b"gfx950" in L.gnn_version()
+    assert L.gnn_last_error() is not None
+
+
+def test_argument_validation_without_gpu():
+    L = _lib.lib()
+    # negative sizes are rejected before any HIP call
+    rc = L.gnn_spmm_csr_f32(None, None, None, -1, 1, 1, None, 1, None, 1, 1, None, 0, 0, None)
+    assert rc == -22 and b"negative" in L.gnn_last_error()
+    with pytest.raises(RuntimeError, match="negative size"):
+        _lib.check(L.gnn_gather_rows_f32(None, 1, None, None, 1, None, -5, 1, None), "gather")
+    # F larger than the row stride
+    rc = L.gnn_spmm_csr_f32(None, None, None, 4, 4, 0, None, 2, None, 8, 4, None, 0, 0, None)
+    assert rc == -22 and b"ldx" in L.gnn_last_error()
+    # zero-size problems are no-ops (nothing launched)
+    assert L.gnn_spmm_csr_f32(None, None, None, 0, 4, 0, None, 8, None, 8, 8, None, 0, 0, None) == 0
+
+
+def test_workspace_and_config():
+    from gnn_amd.custom_sparse_ops import spmm_config
+
+    L = _lib.lib()
+    assert L.gnn_spmm_default_unit_nnz(15809, 1810000, 602) >= 16
+    ws = L.gnn_spmm_workspace_bytes(15809, 1810000, 602, 0)
+    unit = L.gnn_spmm_default_unit_nnz(15809, 1810000, 602)
+    assert ws >= ((1810000 + unit - 1) // unit) * 2 * 604 * 4
+    c = spmm_config(15809, 1810000, 602)
+    assert c["vw"] == 2 and c["g"] * c["nj"] * c["vw"] * c["tiles"] >= 602
+    c = spmm_config(8689, 850000, 1024)
+    assert c["vw"] == 4 and c["g"] * c["nj"] * 4 * c["tiles"] == 1024
+    c = spmm_config(100, 1000, 602, ldx=608)
+    assert c["vw"] == 2  # F itself is not a multiple of 4
+    c = spmm_config(100, 1000, 5000)
+    assert c["tiles"] >= 2 and c["nj"] <= 8
+    assert L.gnn_csr_transpose_workspace_bytes(10, 1000, 50) >= 4000
+    assert L.gnn_segsort_workspace_bytes(100) >= 800
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(RuntimeError, match="missing"):
+        _lib.lib()
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(REPO, "gnn_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(root, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, flags=re.M), f
