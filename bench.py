@@ -1,0 +1,240 @@
+"""Benchmark: Reddit GraphSAGE / LADIES mini-batch training on MI355X (BASELINE.json config 2).
+
+One step = one data-parallel mini-batch training iteration of the reference's hot path
+(main.py:122-170) on a pre-sampled LADIES batch whose operands and index arrays are resident
+in HBM: X0 staging (own-GPU buffer gather + pinned-host rows H2D on a side stream, peer rows
+by RCCL all-to-all when N > 1), 3 HIP aggregation forwards + 2 backwards inside GraphSAGE
+(samp_num 8192, batch 512, nhid 512, orders 1,1,1, F = 602, 41 classes), loss, backward,
+clip_grad_norm_(5), RCCL all-reduce(SUM) of the flat gradient, Adam.
+Synthetic Reddit-shaped graph: Chung-Lu lognormal sigma 1.3, N = 232,965,
+~23.1 M nnz, N(0,1) fp32 features (StandardScaler'd analogue), buffer_size = 0.1.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from gnn_amd import custom_sparse_ops as cso  # noqa: E402
+from gnn_amd import graphs, placement, sampler, staging  # noqa: E402
+from gnn_amd.models import build_model  # noqa: E402
+from gnn_amd.train import Trainer, init_distributed  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batches", type=int, default=4, help="distinct pre-sampled batches per rank (cycled)")
+    ap.add_argument("--model", default="graphsage")
+    ap.add_argument("--samp-num", type=int, default=8192)
+    ap.add_argument("--batch-size", type=int, default=512)
+    ap.add_argument("--nhid", type=int, default=512)
+    ap.add_argument("--buffer-size", type=float, default=0.1)
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--graph", default="reddit", choices=["reddit", "tiny"])
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
+    return ap.parse_args()
+
+
+def sample_batches(args, lap, labels, train, pl, rank, world):
+    batches = sampler.rank_batches(train, args.batch_size, rank, world, iter_num=1)[: args.batches]
+    rs = np.random.RandomState(1234 + rank)
+    seeds = rs.randint(2**31 - 1, size=len(batches))
+    out = []
+    for s, b in zip(seeds, batches):
+        out.append(sampler.ladies_sample_host(int(s), b, np.array([args.samp_num] * 5), lap.shape[0], lap, labels,
+                                              [1, 1, 1], pl.device_id_of_nodes_group[rank],
+                                              pl.idx_of_nodes_on_device_group[rank], None, 1.0, list(range(world))))
+    return out
+
+
+def cpu_baseline(args, hb, feats, num_classes):
+    """Reference CPU path (torch.sparse.mm) full training step on the same batch, rank 0 / N=1."""
+    from oracle.cpu_reference import cpu_inputs, cpu_train_step, torch_spmm
+
+    torch.manual_seed(0)
+    model = build_model(args.model, feats.shape[1], args.nhid, [1, 1, 1], num_classes, 0.1, spmm_fn=torch_spmm)
+    opt = torch.optim.Adam(model.parameters(), lr=args.lr)
+    adjs, x0, sampled, labels = cpu_inputs(hb, feats)
+    cpu_train_step(model, opt, adjs, x0, sampled, labels)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        cpu_train_step(model, opt, adjs, x0, sampled, labels)
+        n += 1
+        if time.perf_counter() - t0 >= args.cpu_baseline_seconds or n >= 50:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "mini-batches/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} full GraphSAGE training steps (torch.sparse.mm fwd/bwd, dense layers, Adam) on "
+                      f"pre-sampled batch 0 (samp {args.samp_num}, bs {args.batch_size}), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank, world, local = init_distributed()
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    t0 = time.time()
+    spec = graphs.REDDIT if args.graph == "reddit" else graphs.TINY
+    A, labels, feats, num_classes, train, valid, test = graphs.make_dataset(spec, seed=0)
+    lap = graphs.row_normalize(A)
+    lap.sum_duplicates()
+    N = A.shape[0]
+    log(f"graph {spec.name}: N={N} nnz={A.nnz} ({time.time() - t0:.1f}s)")
+    k = int(args.buffer_size * N)
+    pl = placement.create_buffer(lap, train, k, list(range(world)), 3, alpha=0)
+    log(f"placement k={k} per GPU ({time.time() - t0:.1f}s)")
+    host_batches = sample_batches(args, lap, labels, train, pl, rank, world)
+    log(f"sampled {len(host_batches)} batches ({time.time() - t0:.1f}s); nnz/batch={host_batches[0].nnz()}")
+
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank)
+    exchange = staging.PeerExchange() if world > 1 else None
+    stager = staging.Stager(store, exchange)
+    plans = [staging.make_plan(hb, store, rank, world) for hb in host_batches]
+    # CSR pieces, labels and sampled_nodes resident in HBM; the operand builder (the
+    # create_coo_tensor kernel) and the backward's transpose run inside every step.
+    dbatches = [hb.to_device(dev, build=False) for hb in host_batches]
+    if args.dump_batch and rank == 0:
+        L0 = host_batches[0].layers
+        np.savez(args.dump_batch, **{f"l{i}_{k}": getattr(L, k) for i, L in enumerate(L0)
+                                     for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
+                 **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
+
+    torch.manual_seed(0)
+    model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1).to(dev)
+    trainer = Trainer(model, args.lr, dev)
+    torch.cuda.synchronize()
+    log(f"setup done ({time.time() - t0:.1f}s); params={trainer.num_params}")
+
+    nb = len(dbatches)
+
+    def run(steps, start, timing=False):
+        staged = stager.issue(plans[start % nb])
+        loss = None
+        for i in range(steps):
+            j = (start + i) % nb
+            nxt = stager.issue(plans[(j + 1) % nb]) if i + 1 < steps else None
+            x0 = staged.wait()
+            db = dbatches[j]
+            adjs = db.build_operands()
+            loss = trainer.step(x0, adjs, db.sampled_nodes, db.labels)
+            staged = nxt
+        return loss
+
+    run(args.warmup, 0)
+    cso.enable_timing(not args.no_roofline)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    loss = run(args.steps, args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    cso.enable_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    recs = cso.take_timing_records()
+    final_loss = float(loss.item()) if loss is not None else float("nan")
+
+    # ---------------------------------------------------------------- roofline
+    by = {}
+    for tag, ms, nbytes in recs:
+        e = by.setdefault(tag, [0.0, 0, 0])
+        e[0] += ms
+        e[1] += nbytes
+        e[2] += 1
+    roof = None
+    spmm_detail = {}
+    if recs:
+        # per call site: tag "fwd"/"bwd" + call order within the step (3 fwd, 2 bwd)
+        per_step = 5
+        site = {}
+        for i, (tag, ms, nbytes) in enumerate(recs):
+            key = f"{tag}{i % per_step}"
+            e = site.setdefault(key, [0.0, 0, 0])
+            e[0] += ms
+            e[1] += nbytes
+            e[2] += 1
+        for key, (ms, nbytes, n) in site.items():
+            spmm_detail[key] = {"avg_us": 1e3 * ms / n, "GB_per_launch": nbytes / n / 1e9,
+                                "GBps": nbytes / (ms * 1e-3) / 1e9}
+        dom = max(site, key=lambda k_: site[k_][0])
+        ms, nbytes, n = site[dom]
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": f"spmm_unit_kernel ({'layer-0 forward' if dom == 'fwd0' else dom}), "
+                          f"avg {1e3 * ms / n:.1f} us/launch over {n} launches, "
+                          f"{nbytes / n / 1e9:.3f} GB algorithmic per launch"}
+        tot_ms = sum(v[0] for v in site.values())
+        tot_b = sum(v[1] for v in site.values())
+        roof["all_spmm_GBps"] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)
+        roof["spmm_ms_per_step"] = round(tot_ms / args.steps, 3)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, host_batches[0], feats, num_classes)
+
+    if rank == 0:
+        value = world * args.steps / elapsed
+        line = {
+            "metric": "mini-batches/sec + SpMM HBM GB/s, Reddit GraphSAGE/LADIES at 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "mini-batches/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (Chung-Lu Reddit-shaped graph, N(0,1) features, random-init GraphSAGE); "
+                    f"{nb} pre-sampled LADIES batches per rank cycled, operands resident in HBM",
+            "config": {"workload": "Reddit GraphSAGE LADIES samp_num=8192 batch_size=512 (BASELINE config 2)",
+                       "model": args.model, "global_batch": args.batch_size * world, "samp_num": args.samp_num,
+                       "nhid": args.nhid, "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
+                       "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
+                       "nnz_per_batch": int(host_batches[0].nnz())},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "spmm_per_callsite": spmm_detail,
+            "final_loss": round(final_loss, 5),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

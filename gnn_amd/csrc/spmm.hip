@@ -185,14 +185,18 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
           const int idx = k + t * P + sub;
           int c;
           float v;
+          // idx may run past the chunk (and past lane 63, where lane selects wrap):
+          // such padded slots get v = 0 and re-read a row already in flight.
           if constexpr (P == 1) {
-            c = readlane_i(mc, idx);  // idx is wave-uniform: scalar row address
-            v = readlane_f(mv, idx);  // lanes >= n hold v = 0
-            if (idx >= n) c = last_c;  // padded slot re-reads a row already in flight
+            c = readlane_i(mc, idx & 63);  // idx is wave-uniform: scalar row address
+            v = readlane_f(mv, idx & 63);
           } else {
-            c = __shfl(mc, idx);
-            v = __shfl(mv, idx);
-            if (idx >= n) c = last_c;
+            c = __shfl(mc, idx & 63);
+            v = __shfl(mv, idx & 63);
+          }
+          if (idx >= n) {
+            c = last_c;
+            v = 0.0f;
           }
           vs[t] = v;
           const float* xr = X + (int64_t)c * ldx;

@@ -54,37 +54,48 @@ class HostBatch:
     def nnz(self) -> int:
         return int(sum(l.colidx.size for l in self.layers if l is not None))
 
-    def to_device(self, device, with_coo: bool = True):
-        """Materialise on the GPU. Returns a DeviceBatch."""
-        from . import custom_sparse_ops as cso
-
+    def to_device(self, device, with_coo: bool = True, build: bool = True):
+        """Materialise on the GPU (H2D of the CSR pieces, labels, sampled_nodes) and, unless
+        build=False, run the operand builder. Returns a DeviceBatch."""
         dev = torch.device(device)
-        adjs = []
-        for L in self.layers:
-            if L is None:
-                adjs.append(None)
-                continue
-            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)
-            op, coo = cso.build_operand(t(L.fullrowptr), t(L.rowptr), t(L.colidx), t(L.normfact),
-                                        L.shape[0], L.shape[1], with_coo=with_coo)
-            if with_coo:
-                a = torch.sparse_coo_tensor(coo, op.val, L.shape, is_coalesced=True)
-                a._gnn_csr = op
-                adjs.append(a)
-            else:
-                adjs.append(op)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)
+        raw = [None if L is None else (t(L.fullrowptr), t(L.rowptr), t(L.colidx), t(L.normfact), L.shape)
+               for L in self.layers]
         sampled = [torch.from_numpy(np.asarray(s, dtype=np.int64)).to(dev, non_blocking=True) for s in self.sampled_nodes]
         labels = torch.from_numpy(self.labels).to(dev, non_blocking=True)
-        return DeviceBatch(self, adjs, sampled, labels)
+        db = DeviceBatch(self, raw, None, sampled, labels)
+        if build:
+            db.build_operands(with_coo=with_coo)
+        return db
 
 
 @dataclass
 class DeviceBatch:
     host: HostBatch
-    adjs: list
+    raw: list            # per layer: device (fullrowptr, rowptr, colidx, normfact, shape) or None
+    adjs: Optional[list]
     sampled_nodes: list
     labels: torch.Tensor
-    staging: object = None  # filled by the feature stager
+
+    def build_operands(self, with_coo: bool = False) -> list:
+        """create_coo_tensor for every layer (stream-ordered on the current stream)."""
+        from . import custom_sparse_ops as cso
+
+        adjs = []
+        for r in self.raw:
+            if r is None:
+                adjs.append(None)
+                continue
+            fr, rp, ci, nf, shape = r
+            op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo)
+            if with_coo:
+                a = torch.sparse_coo_tensor(coo, op.val, shape, is_coalesced=True)
+                a._gnn_csr = op
+                adjs.append(a)
+            else:
+                adjs.append(op)
+        self.adjs = adjs
+        return adjs
 
 
 def column_nnz_counts(U: sp.csr_matrix, num_nodes: int) -> np.ndarray:

@@ -1,0 +1,176 @@
+"""Layer-0 feature staging: assemble X0 for a batch from the placement's three sources.
+
+Reference (main.py:129-134): an uninitialised (n_input x F) tensor filled by masked scatters —
+per source GPU i, ``gpu_buffers[i][idx].to(device)`` (gather on GPU i + P2P copy), then the
+non-buffered rows ``feat_data[idx_cpu].to(device, non_blocking=True)`` from PAGEABLE host
+memory, bracketed by device-wide synchronisations.
+
+Here (DESIGN.md §Feature staging):
+  * X0 is allocated with a padded row stride ``ld`` (602 -> 604 floats: 8-byte aligned rows for
+    the aggregation kernel's vector loads); the model sees the (n_input x F) view.
+  * Own-buffer rows: one gather kernel (gnn_gather_rows_f32) from this GPU's buffer straight
+    into their X0 positions.
+  * Host rows: gathered on the host into a PINNED staging tensor (by the batch producer, off
+    the critical path), then one contiguous hipMemcpyAsync on a side stream, then a scatter
+    kernel into X0 — the side stream runs ahead, overlapping the copy with the previous
+    batch's aggregation kernels; the compute stream waits on an event only when it needs X0.
+  * Peer rows (world_size > 1): exchanged with RCCL all-to-all (``PeerExchange``): each rank
+    gathers the rows its peers asked for from its own buffer, one all_to_all_single moves
+    them over xGMI, and a scatter kernel places them.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import custom_sparse_ops as cso
+
+
+def padded_ld(F: int, align: int = 4) -> int:
+    return (F + align - 1) // align * align
+
+
+class FeatureStore:
+    """Placement-resident features of one rank: its GPU buffer + the host table."""
+
+    def __init__(self, feat_data: torch.Tensor, buffer_nodes: np.ndarray, device, rank: int = 0,
+                 pin_host: bool = False):
+        assert feat_data.dtype == torch.float32 and feat_data.dim() == 2
+        self.device = torch.device(device)
+        self.rank = rank
+        self.F = int(feat_data.shape[1])
+        self.ld = padded_ld(self.F)
+        self.host = feat_data.pin_memory() if pin_host else feat_data
+        idx = torch.from_numpy(np.asarray(buffer_nodes, dtype=np.int64))
+        buf = torch.zeros((len(idx), self.ld), dtype=torch.float32)
+        buf[:, : self.F] = feat_data[idx]
+        self.gpu_buffer = buf.to(self.device)  # (k x ld), row i = node buffer_nodes[i]
+
+    def host_rows_pinned(self, node_ids: np.ndarray) -> torch.Tensor:
+        """Host gather of non-buffered rows into a pinned (n x F) tensor."""
+        n = len(node_ids)
+        out = torch.empty((n, self.F), dtype=torch.float32).pin_memory()
+        if n:
+            torch.index_select(self.host, 0, torch.from_numpy(np.asarray(node_ids, dtype=np.int64)), out=out)
+        return out
+
+
+@dataclass
+class StagePlan:
+    """Host-side description of one batch's X0 assembly (all int64 index arrays)."""
+    n_input: int
+    own_pos: np.ndarray      # X0 rows filled from this rank's buffer
+    own_src: np.ndarray      # their slots in the buffer
+    host_pos: np.ndarray     # X0 rows filled from host memory
+    host_rows: torch.Tensor  # pinned (n_host x F) rows, already gathered on the host
+    peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
+    peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
+    pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos)
+
+
+def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devices=None) -> StagePlan:
+    devices = list(range(world_size)) if devices is None else list(devices)
+    masks = host_batch.input_nodes_mask_on_devices
+    idxs = host_batch.nodes_idx_on_devices
+    own_pos = np.flatnonzero(masks[rank]).astype(np.int64)
+    own_src = np.asarray(idxs[rank], dtype=np.int64)
+    host_pos = np.flatnonzero(host_batch.input_nodes_mask_on_cpu).astype(np.int64)
+    host_rows = store.host_rows_pinned(host_batch.nodes_idx_on_cpu)
+    peer_pos, peer_src = [], []
+    for j in range(world_size):
+        if j == rank:
+            peer_pos.append(np.zeros(0, np.int64))
+            peer_src.append(np.zeros(0, np.int64))
+        else:
+            peer_pos.append(np.flatnonzero(masks[j]).astype(np.int64))
+            peer_src.append(np.asarray(idxs[j], dtype=np.int64))
+    pin = tuple(torch.from_numpy(a).pin_memory() for a in (own_pos, own_src, host_pos))
+    return StagePlan(host_batch.num_input_nodes, own_pos, own_src, host_pos, host_rows, peer_pos, peer_src, pin)
+
+
+class Stager:
+    """Issues X0 assembly on a side stream; ``wait`` hands X0 to the compute stream."""
+
+    def __init__(self, store: FeatureStore, exchange: Optional["PeerExchange"] = None):
+        self.store = store
+        self.device = store.device
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.exchange = exchange
+
+    def issue(self, plan: StagePlan):
+        dev = self.device
+        st = self.stream
+        st.wait_stream(torch.cuda.current_stream(dev))  # inputs produced earlier on compute
+        with torch.cuda.stream(st):
+            x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
+            own_pos, own_src, host_pos = (t.to(dev, non_blocking=True) for t in plan.pinned)
+            host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
+            cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
+            if len(plan.host_pos):
+                cso.gather_rows(host_dev, None, x0[:, : self.store.F], host_pos, n=len(plan.host_pos))
+            if self.exchange is not None:
+                self.exchange.exchange(plan, x0, self.store)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        keep = (own_pos, own_src, host_pos, host_dev)
+        return StagedX0(x0, ev, keep, self.store.F)
+
+
+class StagedX0:
+    def __init__(self, x0, event, keep, F):
+        self._x0 = x0
+        self.event = event
+        self._keep = keep
+        self.F = F
+
+    def wait(self) -> torch.Tensor:
+        """Make the current stream wait for the staging and return the (n x F) view."""
+        cur = torch.cuda.current_stream(self._x0.device)
+        cur.wait_event(self.event)
+        self._x0.record_stream(cur)
+        for t in self._keep:
+            t.record_stream(cur)
+        return self._x0[:, : self.F]
+
+
+class PeerExchange:
+    """All-to-all exchange of buffered rows held by peer GPUs (RCCL over xGMI).
+
+    Rank r needs, from each peer j, the rows at slots ``plan.peer_src[j]`` of j's buffer.
+    1) all_to_all of the per-peer request counts (host-visible: sizes the next two calls),
+    2) all_to_all of the requested slot ids, 3) every rank gathers the requested rows from
+    its own buffer (HIP gather) and 4) one all_to_all_single moves the rows; 5) a scatter
+    kernel drops them at their X0 positions."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore):
+        dist = self.dist
+        dev = x0.device
+        W = self.world
+        send_counts = torch.tensor([len(plan.peer_src[j]) for j in range(W)], dtype=torch.int64, device=dev)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        rc = recv_counts.cpu().tolist()  # small sync: sizes for the variable-size calls
+        sc = send_counts.cpu().tolist()
+        req = torch.from_numpy(np.concatenate(plan.peer_src) if W else np.zeros(0, np.int64)).to(dev)
+        want = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(want, req, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
+        F, ld = store.F, store.ld
+        send_rows = torch.empty((sum(rc), ld), dtype=torch.float32, device=dev)
+        if sum(rc):
+            cso.gather_rows(store.gpu_buffer, want, send_rows, None, n=sum(rc))
+        recv_rows = torch.empty((sum(sc), ld), dtype=torch.float32, device=dev)
+        dist.all_to_all_single(recv_rows, send_rows, output_split_sizes=sc, input_split_sizes=rc, group=self.group)
+        pos = torch.from_numpy(np.concatenate(plan.peer_pos) if W else np.zeros(0, np.int64)).to(dev)
+        if sum(sc):
+            cso.gather_rows(recv_rows, None, x0, pos, n=sum(sc))
