@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--unfused", action="store_true", help="torch elementwise layer tail instead of the HIP one")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     return ap.parse_args()
 
@@ -126,7 +127,7 @@ def main():
                  **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
 
     torch.manual_seed(0)
-    model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1).to(dev)
+    model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
     trainer = Trainer(model, args.lr, dev)
     torch.cuda.synchronize()
     log(f"setup done ({time.time() - t0:.1f}s); params={trainer.num_params}")
@@ -224,7 +225,8 @@ def main():
                        "model": args.model, "global_batch": args.batch_size * world, "samp_num": args.samp_num,
                        "nhid": args.nhid, "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
-                       "nnz_per_batch": int(host_batches[0].nnz())},
+                       "nnz_per_batch": int(host_batches[0].nnz()),
+                       "fused_epilogue": not args.unfused},
             "roofline": roof,
             "cpu_baseline": cpu,
             "spmm_per_callsite": spmm_detail,

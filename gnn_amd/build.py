@@ -8,15 +8,16 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "spmm.hip")
-HDR = os.path.join(REPO, "include", "gnn_spmm.h")
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("spmm.hip", "sage.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("gnn_spmm.h", "gnn_layers.h")] + [
+    os.path.join(HERE, "csrc", "common.h")]
 OUT = os.path.join(HERE, "libgnn_spmm.so")
 ARCH = os.environ.get("GNN_OFFLOAD_ARCH", "gfx950")
 
 
 def _build_id() -> str:
     h = hashlib.sha1()
-    for p in (SRC, HDR):
+    for p in SRCS + HDRS:
         with open(p, "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:12]
@@ -31,7 +32,7 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
                 return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           f"-I{os.path.join(REPO, 'include')}", f'-DGNN_BUILD_ID="{bid}"', "-o", OUT + ".tmp", SRC]
+           f"-I{os.path.join(REPO, 'include')}", f'-DGNN_BUILD_ID="{bid}"', "-o", OUT + ".tmp"] + SRCS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

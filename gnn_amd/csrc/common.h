@@ -1,0 +1,36 @@
+// common.h — shared host helpers of libgnn_spmm.so (error reporting, sizes).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#define GNN_EINVAL (-22)
+
+namespace gnn {
+
+// Records the message for gnn_last_error() (thread-local) and returns `code`.
+int fail(int code, const char* fmt, ...);
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace gnn
+
+#define GNN_REQUIRE(cond, ...)                              \
+  do {                                                      \
+    if (!(cond)) return ::gnn::fail(GNN_EINVAL, __VA_ARGS__); \
+  } while (0)
+
+#define GNN_LAUNCHED(name)                                                                       \
+  do {                                                                                           \
+    hipError_t e_ = hipGetLastError();                                                           \
+    if (e_ != hipSuccess) return ::gnn::fail((int)e_, "%s launch: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+#define GNN_HIP(call, name)                                                                \
+  do {                                                                                     \
+    hipError_t e_ = (call);                                                                \
+    if (e_ != hipSuccess) return ::gnn::fail((int)e_, "%s: %s", name, hipGetErrorString(e_)); \
+  } while (0)

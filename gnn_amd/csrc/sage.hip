@@ -1,0 +1,343 @@
+// sage.hip — fused GraphSAGE / GCN layer epilogue (forward + backward), gfx950.
+//
+// Reference (models.py:16-25, 58-64, 43, 82): after the two linear layers, torch runs
+// cat -> elu -> mean -> var -> sub -> mul(scale) -> rsqrt -> mul -> add(offset) -> dropout,
+// each a separate pass over the (M x 1024) activation, and about twice as many passes in
+// backward. Here one wave owns one row: the row (<= 2048 floats, <= 8 float4 per lane) is
+// read once into registers, ELU'd, reduced twice with wave shuffles (mean, then the centred
+// second moment: the same two-pass variance torch computes), normalised, scaled, dropped
+// out and stored once. Backward re-reads the linear outputs and the saved per-row mean and
+// rstd, regenerates the dropout mask from its counter hash, and writes the two input
+// gradients in one pass; d(scale), d(offset) are column sums reduced per workgroup into a
+// slab and then summed over workgroups in a fixed order (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "common.h"
+#include "gnn_layers.h"
+
+namespace {
+
+using gnn::ceil_div;
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int SN_MAXV = 8;   // float4 per lane: D <= 64 * 4 * 8 = 2048
+constexpr int BWD_MAX_GRID = 512;
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {  // "lowbias32" integer hash
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Keep-mask of inverted dropout for element `idx` (row * D + col): P(keep) = 1 - p.
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, float p) {
+  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ mix32((uint32_t)seed ^ 0x9e3779b9u) ^
+                                                 (uint32_t)(seed >> 32)));
+  return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
+}
+
+__device__ __forceinline__ float elu1(float h) { return h > 0.0f ? h : expm1f(h); }
+__device__ __forceinline__ float elu1_grad(float h) { return h > 0.0f ? 1.0f : expf(h); }
+
+__device__ __forceinline__ f4 load_h(const float* hB, int64_t ldb, int D1, const float* hW, int64_t ldw, int r,
+                                     int c) {
+  return (c < D1) ? *reinterpret_cast<const f4*>(hB + (int64_t)r * ldb + c)
+                  : *reinterpret_cast<const f4*>(hW + (int64_t)r * ldw + (c - D1));
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restrict__ hB, int64_t ldb, int D1,
+                                                            const float* __restrict__ hW, int64_t ldw, int D,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ offset, int M, float p,
+                                                            float inv_keep, uint64_t seed, int training,
+                                                            float* __restrict__ Y, int64_t ldy,
+                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= M) return;
+  f4 o[NV];
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D) {
+      const f4 h = load_h(hB, ldb, D1, hW, ldw, r, c);
+      o[k] = f4{elu1(h.x), elu1(h.y), elu1(h.z), elu1(h.w)};
+      s += (o[k].x + o[k].y) + (o[k].z + o[k].w);
+    } else {
+      o[k] = f4(0.0f);
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.0f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D) {
+      const f4 d = o[k] - mean;
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+    }
+  }
+  const float var = wave_sum(q) / (float)D + 1e-9f;
+  const float rstd = rsqrtf(var);
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D) {
+      const f4 sc = *reinterpret_cast<const f4*>(scale + c);
+      const f4 of = *reinterpret_cast<const f4*>(offset + c);
+      f4 y = (o[k] - mean) * sc * rstd + of;
+      if (training) {
+        const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
+        y.x = keep_elem(seed, e + 0, p) ? y.x * inv_keep : 0.0f;
+        y.y = keep_elem(seed, e + 1, p) ? y.y * inv_keep : 0.0f;
+        y.z = keep_elem(seed, e + 2, p) ? y.z * inv_keep : 0.0f;
+        y.w = keep_elem(seed, e + 3, p) ? y.w * inv_keep : 0.0f;
+      }
+      *reinterpret_cast<f4*>(Y + (int64_t)r * ldy + c) = y;
+    }
+  }
+  if (lane == 0) {
+    mean_out[r] = mean;
+    rstd_out[r] = rstd;
+  }
+}
+
+template <int NV>
+__global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
+    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb, int D1,
+    const float* __restrict__ hW, int64_t ldw, int D, const float* __restrict__ scale,
+    const float* __restrict__ mean, const float* __restrict__ rstd, int M, float p, float inv_keep, uint64_t seed,
+    int training, float* __restrict__ dhB, float* __restrict__ dhW, float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][2][D]
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  f4 ds[NV], db[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    ds[k] = f4(0.0f);
+    db[k] = f4(0.0f);
+  }
+  for (int r = blockIdx.x * 4 + w; r < M; r += gridDim.x * 4) {
+    const float m = mean[r];
+    const float rs = rstd[r];
+    f4 h[NV], xh[NV], gx[NV];
+    float a = 0.0f, b = 0.0f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < D) {
+        h[k] = load_h(hB, ldb, D1, hW, ldw, r, c);
+        const f4 o = f4{elu1(h[k].x), elu1(h[k].y), elu1(h[k].z), elu1(h[k].w)};
+        xh[k] = (o - m) * rs;
+        f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
+        if (training) {
+          const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
+          g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
+          g.y = keep_elem(seed, e + 1, p) ? g.y * inv_keep : 0.0f;
+          g.z = keep_elem(seed, e + 2, p) ? g.z * inv_keep : 0.0f;
+          g.w = keep_elem(seed, e + 3, p) ? g.w * inv_keep : 0.0f;
+        }
+        db[k] += g;
+        ds[k] += g * xh[k];
+        gx[k] = g * *reinterpret_cast<const f4*>(scale + c);
+        const f4 gxx = gx[k] * xh[k];
+        a += (gx[k].x + gx[k].y) + (gx[k].z + gx[k].w);
+        b += (gxx.x + gxx.y) + (gxx.z + gxx.w);
+      } else {
+        h[k] = xh[k] = gx[k] = f4(0.0f);
+      }
+    }
+    a = wave_sum(a) / (float)D;
+    b = wave_sum(b) / (float)D;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < D) {
+        const f4 dxo = rs * (gx[k] - a - xh[k] * b);
+        const f4 dh = f4{dxo.x * elu1_grad(h[k].x), dxo.y * elu1_grad(h[k].y), dxo.z * elu1_grad(h[k].z),
+                         dxo.w * elu1_grad(h[k].w)};
+        if (c < D1) {
+          *reinterpret_cast<f4*>(dhB + (int64_t)r * D1 + c) = dh;
+        } else {
+          *reinterpret_cast<f4*>(dhW + (int64_t)r * (D - D1) + (c - D1)) = dh;
+        }
+      }
+    }
+  }
+  // workgroup column sums of d(scale) and d(offset) -> partial[blockIdx.x][2][D]
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = (lane + 64 * k) * 4;
+    if (c < D) {
+      *reinterpret_cast<f4*>(red + (w * 2 + 0) * D + c) = ds[k];
+      *reinterpret_cast<f4*>(red + (w * 2 + 1) * D + c) = db[k];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += 256) {
+    const int half = i / D, c = i % D;
+    float s = 0.0f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) s += red[(ww * 2 + half) * D + c];
+    partial[(int64_t)blockIdx.x * 2 * D + i] = s;
+  }
+}
+
+// Column sums over the G workgroup partials: a workgroup owns 64 of the 2D columns; its 4
+// waves take interleaved quarters of the partial rows (8 loads in flight per lane), and the
+// quarters are added in a fixed order through LDS (deterministic).
+__global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float* __restrict__ partial, int G, int D,
+                                                                     float* __restrict__ dscale,
+                                                                     float* __restrict__ doffset) {
+  __shared__ float q[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  float s = 0.0f;
+  if (i < 2 * D) {
+    const int64_t stride = 2 * (int64_t)D;
+    int g = w;
+    float a[8];
+    for (; g + 28 < G; g += 32) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = partial[(int64_t)(g + 4 * k) * stride + i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += a[k];
+    }
+    for (; g < G; g += 4) s += partial[(int64_t)g * stride + i];
+  }
+  q[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && i < 2 * D) {
+    const float t = (q[0][lane] + q[1][lane]) + (q[2][lane] + q[3][lane]);
+    if (i < D) {
+      dscale[i] = t;
+    } else {
+      doffset[i - D] = t;
+    }
+  }
+}
+
+using FwdFn = void (*)(const float*, int64_t, int, const float*, int64_t, int, const float*, const float*, int, float,
+                       float, uint64_t, int, float*, int64_t, float*, float*);
+using BwdFn = void (*)(const float*, int64_t, const float*, int64_t, int, const float*, int64_t, int, const float*,
+                       const float*, const float*, int, float, float, uint64_t, int, float*, float*, float*);
+
+FwdFn fwd_fn(int nv) {
+  switch (nv) {
+    case 1: return &sage_norm_fwd_kernel<1>;
+    case 2: return &sage_norm_fwd_kernel<2>;
+    case 3: return &sage_norm_fwd_kernel<3>;
+    case 4: return &sage_norm_fwd_kernel<4>;
+    case 5: return &sage_norm_fwd_kernel<5>;
+    case 6: return &sage_norm_fwd_kernel<6>;
+    case 7: return &sage_norm_fwd_kernel<7>;
+    case 8: return &sage_norm_fwd_kernel<8>;
+    default: return nullptr;
+  }
+}
+
+BwdFn bwd_fn(int nv) {
+  switch (nv) {
+    case 1: return &sage_norm_bwd_kernel<1>;
+    case 2: return &sage_norm_bwd_kernel<2>;
+    case 3: return &sage_norm_bwd_kernel<3>;
+    case 4: return &sage_norm_bwd_kernel<4>;
+    case 5: return &sage_norm_bwd_kernel<5>;
+    case 6: return &sage_norm_bwd_kernel<6>;
+    case 7: return &sage_norm_bwd_kernel<7>;
+    case 8: return &sage_norm_bwd_kernel<8>;
+    default: return nullptr;
+  }
+}
+
+int check_shapes(const char* fn, int64_t D1, int64_t D2, int64_t M, const void* hB, int64_t ldb, const void* hW,
+                 int64_t ldw) {
+  GNN_REQUIRE(M >= 0 && D1 >= 0 && D2 >= 0, "%s: negative size", fn);
+  GNN_REQUIRE(M < INT_MAX, "%s: M too large", fn);
+  GNN_REQUIRE(D1 % 4 == 0 && D2 % 4 == 0, "%s: D1 and D2 must be multiples of 4", fn);
+  GNN_REQUIRE(D1 + D2 > 0 && D1 + D2 <= SN_MAXV * 256, "%s: D = %lld outside (0, 2048]", fn,
+              (long long)(D1 + D2));
+  GNN_REQUIRE(D1 == 0 || (hB && ldb % 4 == 0 && (uintptr_t)hB % 16 == 0), "%s: hB must be 16-byte aligned rows", fn);
+  GNN_REQUIRE(D2 == 0 || (hW && ldw % 4 == 0 && (uintptr_t)hW % 16 == 0), "%s: hW must be 16-byte aligned rows", fn);
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float* hW, int64_t ldw, int64_t D2,
+                          const float* scale, const float* offset, int64_t M, float p_drop, uint64_t seed,
+                          int training, float* Y, int64_t ldy, float* mean_out, float* rstd_out, void* stream) {
+  int rc = check_shapes("gnn_sage_norm_fwd_f32", D1, D2, M, hB, ldb, hW, ldw);
+  if (rc) return rc;
+  if (M == 0) return 0;
+  GNN_REQUIRE(scale && offset && Y && mean_out && rstd_out, "gnn_sage_norm_fwd_f32: NULL pointer");
+  GNN_REQUIRE(ldy % 4 == 0 && (uintptr_t)Y % 16 == 0, "gnn_sage_norm_fwd_f32: Y must be 16-byte aligned rows");
+  GNN_REQUIRE(p_drop >= 0.0f && p_drop < 1.0f, "gnn_sage_norm_fwd_f32: p_drop must be in [0, 1)");
+  const int D = (int)(D1 + D2);
+  const int nv = (int)ceil_div(D, 256);
+  hipStream_t st = (hipStream_t)stream;
+  const float inv_keep = 1.0f / (1.0f - p_drop);
+  hipLaunchKernelGGL(fwd_fn(nv), dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, st, hB ? hB : hW, ldb, (int)D1, hW,
+                     ldw, D, scale, offset, (int)M, p_drop, inv_keep, seed, training, Y, ldy, mean_out, rstd_out);
+  GNN_LAUNCHED("sage_norm_fwd_kernel");
+  return 0;
+}
+
+size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
+  const int64_t G = M <= 0 ? 1 : (ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID);
+  return gnn::align_up((size_t)G * 2 * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
+}
+
+int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
+                          int64_t ldw, int64_t D2, const float* scale, const float* mean, const float* rstd, int64_t M,
+                          float p_drop, uint64_t seed, int training, float* dhB, float* dhW, float* dscale,
+                          float* doffset, void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_shapes("gnn_sage_norm_bwd_f32", D1, D2, M, hB, ldb, hW, ldw);
+  if (rc) return rc;
+  GNN_REQUIRE(scale && dscale && doffset, "gnn_sage_norm_bwd_f32: NULL pointer");
+  GNN_REQUIRE(p_drop >= 0.0f && p_drop < 1.0f, "gnn_sage_norm_bwd_f32: p_drop must be in [0, 1)");
+  const int D = (int)(D1 + D2);
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) {
+    GNN_HIP(hipMemsetAsync(dscale, 0, (size_t)D * 4, st), "dscale memset");
+    GNN_HIP(hipMemsetAsync(doffset, 0, (size_t)D * 4, st), "doffset memset");
+    return 0;
+  }
+  GNN_REQUIRE(gY && mean && rstd && (D1 == 0 || dhB) && (D2 == 0 || dhW), "gnn_sage_norm_bwd_f32: NULL pointer");
+  GNN_REQUIRE(ldg % 4 == 0 && (uintptr_t)gY % 16 == 0, "gnn_sage_norm_bwd_f32: gY must be 16-byte aligned rows");
+  GNN_REQUIRE(D1 == 0 || (uintptr_t)dhB % 16 == 0, "gnn_sage_norm_bwd_f32: dhB not 16-byte aligned");
+  GNN_REQUIRE(D2 == 0 || (uintptr_t)dhW % 16 == 0, "gnn_sage_norm_bwd_f32: dhW not 16-byte aligned");
+  GNN_REQUIRE(workspace && workspace_bytes >= gnn_sage_norm_bwd_workspace_bytes(M, D),
+              "gnn_sage_norm_bwd_f32: workspace too small");
+  const int nv = (int)ceil_div(D, 256);
+  const int64_t G = ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID;
+  const float inv_keep = 1.0f / (1.0f - p_drop);
+  float* partial = (float*)workspace;
+  hipLaunchKernelGGL(bwd_fn(nv), dim3((unsigned)G), dim3(256), (size_t)8 * D * sizeof(float), st, gY, ldg,
+                     hB ? hB : hW, ldb, (int)D1, hW, ldw, D, scale, mean, rstd, (int)M, p_drop, inv_keep, seed,
+                     training, dhB ? dhB : dhW, dhW, partial);
+  GNN_LAUNCHED("sage_norm_bwd_kernel");
+  sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(2 * D, 64)), dim3(256), 0, st>>>(partial, (int)G, D, dscale,
+                                                                                          doffset);
+  GNN_LAUNCHED("sage_norm_bwd_finalize_kernel");
+  return 0;
+}
+
+}  // extern "C"

@@ -27,19 +27,18 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <string>
 
 #include "gnn_spmm.h"
+#include "common.h"
 
 #ifndef GNN_BUILD_ID
 #define GNN_BUILD_ID "dev"
 #endif
 
-namespace {
-
+namespace gnn {
 thread_local std::string g_err;
-thread_local hipEvent_t g_ev_start = nullptr;
-thread_local hipEvent_t g_ev_stop = nullptr;
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -50,26 +49,17 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
+}  // namespace gnn
 
-#define GNN_REQUIRE(cond, ...)                 \
-  do {                                         \
-    if (!(cond)) return fail(GNN_EINVAL, __VA_ARGS__); \
-  } while (0)
+namespace {
 
-#define GNN_LAUNCHED(name)                                                        \
-  do {                                                                            \
-    hipError_t e_ = hipGetLastError();                                            \
-    if (e_ != hipSuccess) return fail((int)e_, "%s launch: %s", name, hipGetErrorString(e_)); \
-  } while (0)
+using gnn::align_up;
+using gnn::ceil_div;
+using gnn::fail;
+using gnn::g_err;
 
-#define GNN_HIP(call, name)                                                       \
-  do {                                                                            \
-    hipError_t e_ = (call);                                                       \
-    if (e_ != hipSuccess) return fail((int)e_, "%s: %s", name, hipGetErrorString(e_)); \
-  } while (0)
-
-inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
-inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+thread_local hipEvent_t g_ev_start = nullptr;
+thread_local hipEvent_t g_ev_stop = nullptr;
 
 // ---------------------------------------------------------------------------------
 // Vector types: clang ext vectors give global_load_dwordx2/x4 and per-lane packed FMA.
@@ -239,7 +229,8 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
 }
 
 // Adds the unit pieces of every row that straddles a unit boundary, in unit order.
-// Grid: (ceil(M/4), column chunks of 64*VW); one wave per (row, column chunk).
+// Grid-stride over rows (a capped grid: most rows are not split and exit at once); a wave
+// sums one split row, its lanes spanning the columns.
 template <int VW>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int* __restrict__ rowptr, int M, int S,
@@ -247,41 +238,48 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
     float* __restrict__ Y, int64_t ldy, int F) {
   using V = typename Vec<VW>::T;
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= M) return;
-  const int rb = rowptr[r];
-  const int re = rowptr[r + 1];
-  if (re == rb) return;
-  const int u0 = rb / S;
-  const int u1 = (re - 1) / S;
-  if (u0 == u1) return;
-  const int cc = (blockIdx.y * 64 + lane) * VW;
-  if (cc >= F) return;
-  V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
-  int u = u0 + 1;
-  for (; u + 4 <= u1 + 1; u += 4) {
-    const V a0 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 0) * 2) * ldslab + cc);
-    const V a1 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 1) * 2) * ldslab + cc);
-    const V a2 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 2) * 2) * ldslab + cc);
-    const V a3 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 3) * 2) * ldslab + cc);
-    s += a0;
-    s += a1;
-    s += a2;
-    s += a3;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < M; r += gridDim.x * 4) {
+    const int rb = rowptr[r];
+    const int re = rowptr[r + 1];
+    if (re == rb) continue;
+    const int u0 = rb / S;
+    const int u1 = (re - 1) / S;
+    if (u0 == u1) continue;
+    for (int cc = lane * VW; cc < F; cc += 64 * VW) {
+      V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
+      int u = u0 + 1;
+      for (; u + 4 <= u1 + 1; u += 4) {
+        const V a0 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 0) * 2) * ldslab + cc);
+        const V a1 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 1) * 2) * ldslab + cc);
+        const V a2 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 2) * 2) * ldslab + cc);
+        const V a3 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 3) * 2) * ldslab + cc);
+        s += a0;
+        s += a1;
+        s += a2;
+        s += a3;
+      }
+      for (; u <= u1; ++u) s += *reinterpret_cast<const V*>(slab + ((int64_t)u * 2) * ldslab + cc);
+      *reinterpret_cast<V*>(Y + (int64_t)r * ldy + cc) = s;
+    }
   }
-  for (; u <= u1; ++u) s += *reinterpret_cast<const V*>(slab + ((int64_t)u * 2) * ldslab + cc);
-  *reinterpret_cast<V*>(Y + (int64_t)r * ldy + cc) = s;
 }
 
 // ---------------------------------------------------------------------------------
 // Operand builder: value = (float)((1.0 / full_degree(row)) * (double)normfact[col]),
 // the formula of cuda_spmm.cu:800 evaluated in double. One wave per row.
 // ---------------------------------------------------------------------------------
+__device__ __forceinline__ void cmpx_reg(int& k, float& v, int lane, int mask);
+
+// Also restores the coalesced (column-ascending) order the reference gets from
+// .coalesce(): rows found unsorted are sorted here when short (<= 64 entries, in
+// registers) or queued for the segmented sorters (counters[0]: <= SEG_BLOCK_LDS entries,
+// counters[1]: longer). Sorted rows — scipy's slicing output — cost nothing extra.
 template <typename CT>
 __global__ __launch_bounds__(256) void build_operand_kernel(
     const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
     const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
-    int* __restrict__ out_col, float* __restrict__ out_val) {
+    int* __restrict__ out_col, float* __restrict__ out_val,
+    int* __restrict__ counters, int* __restrict__ list_mid, int* __restrict__ list_long, int block_cap) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= nrows) return;
@@ -289,10 +287,37 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
   const int e = rowptr[r + 1];
   if (b == e) return;
   const double inv = 1.0 / (double)(fullrowptr[r + 1] - fullrowptr[r]);
+  bool bad = false;
   for (int i = b + lane; i < e; i += 64) {
     const int c = (int)colidx[i];
+    if (i + 1 < e) bad |= c > (int)colidx[i + 1];
     out_col[i] = c;
     out_val[i] = (float)(inv * (double)normfact[c]);
+  }
+  if (__ballot(bad) == 0ull) return;
+  const int L = e - b;
+  if (L <= 64) {
+    // this wave wrote the row above; re-read it (same lanes' own stores) and sort in registers
+    int k = INT_MAX;
+    float v = 0.0f;
+    if (lane < L) {
+      k = (int)colidx[b + lane];
+      v = (float)(inv * (double)normfact[k]);
+    }
+    for (int size = 2; size <= 64; size <<= 1) {
+      cmpx_reg(k, v, lane, size - 1);
+      for (int d = size >> 2; d >= 1; d >>= 1) cmpx_reg(k, v, lane, d);
+    }
+    if (lane < L) {
+      out_col[b + lane] = k;
+      out_val[b + lane] = v;
+    }
+  } else if (lane == 0) {
+    if (L <= block_cap) {
+      list_mid[atomicAdd(&counters[0], 1)] = r;
+    } else {
+      list_long[atomicAdd(&counters[1], 1)] = r;
+    }
   }
 }
 
@@ -406,6 +431,111 @@ __global__ __launch_bounds__(256) void transpose_scatter_kernel(
     const int pos = atomicAdd(&cursor[col[i]], 1);
     tr_col[pos] = r;
     tr_val[pos] = val[i];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Tiled transpose (K <= TR_MAX_K): a stable counting sort by column with no global atomics
+// and no sort pass. The nonzeros are cut into T tiles of TS consecutive entries (CSR order).
+//  1. tr_tile_hist:   per tile, an LDS histogram of its columns -> hist[t][0..K).
+//  2. tr_col_prefix:  per column, exclusive prefix of hist over tiles (in place) -> the
+//                     offset of tile t's first entry inside output row c; totals -> cnt.
+//     (then scan_exclusive_kernel turns cnt into tr_rowptr.)
+//  3. tr_tile_scatter: per tile, LDS cursors cur[c] = tr_rowptr[c] + hist[t][c]; ONE wave
+//                     walks the tile's rows in order, one row segment per LDS access, so
+//                     the lanes of an access hold distinct columns and rows are placed in
+//                     ascending order: the result is the canonical (coalesced) transpose.
+// ---------------------------------------------------------------------------------
+constexpr int TR_MAX_K = 32 * 1024;   // cursor / histogram array in LDS (128 KiB)
+constexpr int TR_MAX_TS = 4 * 1024;   // tile entries preloaded in LDS (32 KiB)
+
+__global__ __launch_bounds__(256) void tr_tile_hist_kernel(const int* __restrict__ col, int nnz, int TS, int K,
+                                                           int* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int lds_i[];
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < K; c += 256) lds_i[c] = 0;
+  __syncthreads();
+  const int b = t * TS;
+  const int e = min(b + TS, nnz);
+  for (int i = b + threadIdx.x; i < e; i += 256) atomicAdd(&lds_i[col[i]], 1);
+  __syncthreads();
+  int* h = hist + (int64_t)t * K;
+  for (int c = threadIdx.x; c < K; c += 256) h[c] = lds_i[c];
+}
+
+__global__ __launch_bounds__(256) void tr_col_prefix_kernel(int* __restrict__ hist, int T, int K,
+                                                            int* __restrict__ cnt) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= K) return;
+  int run = 0;
+  int t = 0;
+  for (; t + 4 <= T; t += 4) {
+    const int64_t o = (int64_t)t * K + c;
+    const int h0 = hist[o], h1 = hist[o + K], h2 = hist[o + 2 * (int64_t)K], h3 = hist[o + 3 * (int64_t)K];
+    hist[o] = run;
+    hist[o + K] = run + h0;
+    hist[o + 2 * (int64_t)K] = run + h0 + h1;
+    hist[o + 3 * (int64_t)K] = run + h0 + h1 + h2;
+    run += h0 + h1 + h2 + h3;
+  }
+  for (; t < T; ++t) {
+    const int64_t o = (int64_t)t * K + c;
+    const int h = hist[o];
+    hist[o] = run;
+    run += h;
+  }
+  cnt[c] = run;
+}
+
+__global__ __launch_bounds__(256) void tr_tile_scatter_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val, int M, int nnz,
+    int TS, int K, const int* __restrict__ hist, const int* __restrict__ tr_rowptr, int* __restrict__ tr_col,
+    float* __restrict__ tr_val) {
+  // LDS: cur[K] cursors, then the tile's columns and values (preloaded by all 4 waves so
+  // the ordered walk below reads only LDS and registers).
+  extern __shared__ __attribute__((aligned(16))) int cur[];
+  int* tcol = cur + ((K + 3) & ~3);
+  float* tval = reinterpret_cast<float*>(tcol + TS);
+  const int t = blockIdx.x;
+  const int b = t * TS;
+  const int e = min(b + TS, nnz);
+  const int* h = hist + (int64_t)t * K;
+  for (int c = threadIdx.x; c < K; c += 256) cur[c] = tr_rowptr[c] + h[c];
+  for (int i = b + threadIdx.x; i < e; i += 256) {
+    tcol[i - b] = col[i];
+    tval[i - b] = val[i];
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  // first row with an entry at position >= b; row ends rowptr[r+1..r+64] held in a register
+  int r = wave_first_true(0, M, lane, [&](int rr) { return rowptr[rr + 1] > b; });
+  int wbase = r;
+  int rp = rowptr[min(r + 1 + lane, M)];
+  for (int base = b; base < e; base += 64) {
+    const int i = base + lane;
+    const bool valid = i < e;
+    const int c = valid ? tcol[i - b] : 0;
+    const float v = valid ? tval[i - b] : 0.0f;
+    const int last = min(base + 64, e);  // one past the chunk's last entry
+    bool todo = valid;
+    while (true) {
+      if (r - wbase >= 64) {
+        wbase = r;
+        rp = rowptr[min(r + 1 + lane, M)];
+      }
+      const int rend = readlane_i(rp, r - wbase);  // rowptr[r + 1], wave-uniform
+      const bool mine = todo && i < rend;
+      if (mine) {
+        const int p = cur[c];
+        cur[c] = p + 1;
+        tr_col[p] = r;
+        tr_val[p] = v;
+      }
+      todo = todo && !mine;
+      if (rend >= last) break;  // row r continues into (or ends at) the next chunk
+      ++r;
+    }
   }
 }
 
@@ -644,11 +774,14 @@ int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
 }
 
 int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
-  (void)M;
   (void)F;
-  // Aim for >= ~16k units (64 waves per CU) so the dispatcher can balance power-law
-  // rows; keep units >= 16 nonzeros so the per-unit search and the slab stay small.
-  int64_t s = ceil_div(nnz, 16384);
+  // Units are equal-sized (S nonzeros), so ~4k of them (2 per wave slot of the chip at 8
+  // waves/CU) already balance power-law rows. Bigger units cut fewer rows: a row is split
+  // (and pays a slab round trip + the combine pass) with probability ~ mean_len / S, so S
+  // is kept >= 4 x the mean row length when that still leaves >= 2k units.
+  int64_t s = ceil_div(nnz, 4096);
+  const int64_t mean_len = M > 0 ? ceil_div(nnz, M) : 1;
+  if (s < 4 * mean_len && ceil_div(nnz, 4 * mean_len) >= 2048) s = 4 * mean_len;
   if (s < 16) s = 16;
   if (s > 4096) s = 4096;
   return s;
@@ -724,22 +857,46 @@ MainFn select_main(const SpmmCfg& c) {
   }
 }
 
+void tr_tiles(int64_t nnz, int64_t& TS, int64_t& T) {
+  TS = ceil_div(nnz, 256);
+  if (TS < 1024) TS = 1024;
+  if (TS > TR_MAX_TS) TS = TR_MAX_TS;
+  T = nnz > 0 ? ceil_div(nnz, TS) : 0;
+}
+
 size_t segsort_ws(int64_t nseg) { return 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * 4, 256) * 2; }
+
+struct SegLists {
+  int* counters;
+  int* list_mid;
+  int* list_long;
+};
+
+SegLists seg_lists(void* ws, int64_t nseg) {
+  char* w = (char*)ws;
+  return SegLists{(int*)w, (int*)(w + 256), (int*)(w + 256 + align_up((size_t)(nseg > 0 ? nseg : 1) * 4, 256))};
+}
+
+// Sort the queued segments: the workgroup (LDS) sorter for counters[0] entries, the
+// global-memory sorter for counters[1]. Small grids: they loop over the (usually empty)
+// lists, reading the counts on the device (no host synchronisation).
+int run_list_sorters(const int* ptr, int* key, float* val, const SegLists& l, hipStream_t st) {
+  segsort_block_kernel<<<dim3(16), dim3(1024), 0, st>>>(ptr, key, val, l.counters, l.list_mid);
+  GNN_LAUNCHED("segsort_block_kernel");
+  segsort_global_kernel<<<dim3(4), dim3(1024), 0, st>>>(ptr, key, val, l.counters, l.list_long);
+  GNN_LAUNCHED("segsort_global_kernel");
+  return 0;
+}
 
 int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hipStream_t st) {
   if (nseg <= 0) return 0;
-  char* w = (char*)ws;
-  int* counters = (int*)w;
-  int* list_mid = (int*)(w + 256);
-  int* list_long = (int*)(w + 256 + align_up((size_t)nseg * 4, 256));
-  GNN_HIP(hipMemsetAsync(counters, 0, 16, st), "segsort counters memset");
-  segsort_wave_kernel<<<dim3((unsigned)ceil_div(nseg, 4)), dim3(256), 0, st>>>(ptr, (int)nseg, key, val, counters,
-                                                                            list_mid, list_long);
+  const SegLists l = seg_lists(ws, nseg);
+  GNN_HIP(hipMemsetAsync(l.counters, 0, 16, st), "segsort counters memset");
+  segsort_wave_kernel<<<dim3((unsigned)ceil_div(nseg, 4)), dim3(256), 0, st>>>(ptr, (int)nseg, key, val, l.counters,
+                                                                            l.list_mid, l.list_long);
   GNN_LAUNCHED("segsort_wave_kernel");
-  segsort_block_kernel<<<dim3(256), dim3(1024), 0, st>>>(ptr, key, val, counters, list_mid);
-  GNN_LAUNCHED("segsort_block_kernel");
-  segsort_global_kernel<<<dim3(16), dim3(1024), 0, st>>>(ptr, key, val, counters, list_long);
-  GNN_LAUNCHED("segsort_global_kernel");
+  int rc = run_list_sorters(ptr, key, val, l, st);
+  if (rc) return rc;
   return 0;
 }
 
@@ -810,7 +967,7 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
   GNN_LAUNCHED("spmm_unit_kernel");
   if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
-    const dim3 g2((unsigned)ceil_div(M, 4), (unsigned)ceil_div(F, 64 * c.vw));
+    const dim3 g2((unsigned)std::min<int64_t>(ceil_div(M, 4), 512));
     switch (c.vw) {
       case 4:
         spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
@@ -842,22 +999,27 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
   GNN_REQUIRE(workspace && workspace_bytes >= segsort_ws(nrows), "gnn_build_operand_f32: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)ceil_div(nrows, 4));
+  const SegLists l = seg_lists(workspace, nrows);
+  GNN_HIP(hipMemsetAsync(l.counters, 0, 16, st), "operand sort-list counters memset");
   switch (colidx_bytes) {
     case 2:
       build_operand_kernel<int16_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
+                                                                l.list_long, SEG_BLOCK_LDS);
       break;
     case 4:
       build_operand_kernel<int32_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
+                                                                l.list_long, SEG_BLOCK_LDS);
       break;
     default:
       build_operand_kernel<int64_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
+                                                                l.list_long, SEG_BLOCK_LDS);
       break;
   }
   GNN_LAUNCHED("build_operand_kernel");
-  int rc = run_segsort(rowptr, nrows, csr_col, csr_val, workspace, st);
+  int rc = run_list_sorters(rowptr, csr_col, csr_val, l, st);
   if (rc) return rc;
   if (coo_indices) {
     csr_to_coo_indices_kernel<<<grid, dim3(256), 0, st>>>(rowptr, csr_col, (int)nrows, nnz, coo_indices);
@@ -885,8 +1047,12 @@ int gnn_coo_to_csr(const int64_t* row, const int64_t* col, int64_t nnz, int64_t 
 
 size_t gnn_csr_transpose_workspace_bytes(int64_t M, int64_t K, int64_t nnz) {
   (void)M;
-  (void)nnz;
-  return align_up((size_t)(K > 0 ? K : 1) * 4, 256) + segsort_ws(K);
+  const size_t fallback = align_up((size_t)(K > 0 ? K : 1) * 4, 256) + segsort_ws(K);
+  if (K > TR_MAX_K) return fallback;
+  int64_t TS = 0, T = 0;
+  tr_tiles(nnz, TS, T);
+  const size_t tiled = align_up((size_t)T * (size_t)K * 4, 256) + align_up((size_t)(K > 0 ? K : 1) * 4, 256);
+  return tiled > fallback ? tiled : fallback;
 }
 
 int gnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val, int64_t M, int64_t K, int64_t nnz,
@@ -905,6 +1071,33 @@ int gnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* va
   GNN_REQUIRE(workspace && workspace_bytes >= gnn_csr_transpose_workspace_bytes(M, K, nnz),
               "gnn_csr_transpose: workspace too small");
   char* w = (char*)workspace;
+  if (K <= TR_MAX_K) {
+    int64_t TS = 0, T = 0;
+    tr_tiles(nnz, TS, T);
+    int* hist = (int*)w;
+    int* cnt = (int*)(w + align_up((size_t)T * (size_t)K * 4, 256));
+    const size_t lds = (size_t)K * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+      GNN_HIP(hipFuncSetAttribute((const void*)tr_tile_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  TR_MAX_K * 4), "hipFuncSetAttribute(tr_tile_hist)");
+      GNN_HIP(hipFuncSetAttribute((const void*)tr_tile_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  TR_MAX_K * 4 + TR_MAX_TS * 8), "hipFuncSetAttribute(tr_tile_scatter)");
+      attr_set = true;
+    }
+    tr_tile_hist_kernel<<<dim3((unsigned)T), dim3(256), lds, st>>>(col, (int)nnz, (int)TS, (int)K, hist);
+    GNN_LAUNCHED("tr_tile_hist_kernel");
+    tr_col_prefix_kernel<<<dim3((unsigned)ceil_div(K, 256)), dim3(256), 0, st>>>(hist, (int)T, (int)K, cnt);
+    GNN_LAUNCHED("tr_col_prefix_kernel");
+    scan_exclusive_kernel<<<dim3(1), dim3(1024), 0, st>>>(cnt, (int)K, tr_rowptr, nullptr);
+    GNN_LAUNCHED("scan_exclusive_kernel");
+    const size_t lds3 = (size_t)((K + 3) & ~3) * 4 + (size_t)TS * 8;
+    tr_tile_scatter_kernel<<<dim3((unsigned)T), dim3(256), lds3, st>>>(rowptr, col, val, (int)M, (int)nnz, (int)TS,
+                                                                     (int)K, hist, tr_rowptr, tr_col, tr_val);
+    GNN_LAUNCHED("tr_tile_scatter_kernel");
+    return 0;
+  }
+  // Large K: atomic slot claim + segmented sort (also canonical and deterministic).
   int* cnt = (int*)w;
   void* ssws = w + align_up((size_t)K * 4, 256);
   GNN_HIP(hipMemsetAsync(cnt, 0, (size_t)K * 4, st), "transpose count memset");

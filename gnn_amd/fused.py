@@ -1,0 +1,116 @@
+"""Fused layer epilogue of GraphSAGE / GCN (HIP, include/gnn_layers.h) as an autograd op.
+
+``sage_norm(hB, hW, scale, offset, p, training)`` computes, per row,
+    dropout_p( (elu(cat[hB, hW]) - mean) * scale * rsqrt(var + 1e-9) + offset )
+which is GraphSageConvolution.forward's tail (models.py:18-25) plus the dropout that
+GraphSage.forward applies to every layer output (models.py:43); with hB = None it is
+GraphConvolution's (models.py:58-64, 82). One HIP pass forward, one (+ a column reduction)
+backward. Dropout masks: a counter hash of (seed, element) with the seed drawn from torch's
+CPU generator, so torch.manual_seed makes runs reproducible; the mask stream differs from
+torch's Philox stream (same distribution).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class SageNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hB, hW, scale, offset, p: float, training: bool, seed: int):
+        for t in (hW, scale, offset) + ((hB,) if hB is not None else ()):
+            if not t.is_cuda:
+                raise RuntimeError("sage_norm: tensors must be CUDA tensors")
+            if t.dtype != torch.float32:
+                raise RuntimeError("sage_norm: tensors must be float32")
+        hW = hW.contiguous()
+        hB = hB.contiguous() if hB is not None else None
+        M, D2 = hW.shape
+        D1 = 0 if hB is None else hB.shape[1]
+        D = D1 + D2
+        dev = hW.device
+        scale = scale.contiguous()
+        offset = offset.contiguous()
+        Y = torch.empty((M, D), dtype=torch.float32, device=dev)
+        mean = torch.empty(M, dtype=torch.float32, device=dev)
+        rstd = torch.empty(M, dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        _lib.check(L.gnn_sage_norm_fwd_f32(_ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(scale), _ptr(offset), M,
+                                           float(p), seed, int(training), _ptr(Y), D, _ptr(mean), _ptr(rstd),
+                                           _stream(dev)), "gnn_sage_norm_fwd_f32")
+        ctx.save_for_backward(hB if hB is not None else hW, hW, scale, mean, rstd)
+        ctx.has_b = hB is not None
+        ctx.cfg = (float(p), int(training), int(seed))
+        return Y
+
+    @staticmethod
+    def backward(ctx, gY):
+        hB, hW, scale, mean, rstd = ctx.saved_tensors
+        if not ctx.has_b:
+            hB = None
+        p, training, seed = ctx.cfg
+        gY = gY.contiguous()
+        M, D2 = hW.shape
+        D1 = 0 if hB is None else hB.shape[1]
+        dev = hW.device
+        dhB = torch.empty_like(hB) if hB is not None else None
+        dhW = torch.empty_like(hW)
+        dscale = torch.empty(D1 + D2, dtype=torch.float32, device=dev)
+        doffset = torch.empty(D1 + D2, dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        wsb = L.gnn_sage_norm_bwd_workspace_bytes(M, D1 + D2)
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        _lib.check(L.gnn_sage_norm_bwd_f32(_ptr(gY), D1 + D2, _ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(scale),
+                                           _ptr(mean), _ptr(rstd), M, p, seed, training, _ptr(dhB), _ptr(dhW),
+                                           _ptr(dscale), _ptr(doffset), _ptr(ws), wsb, _stream(dev)),
+                   "gnn_sage_norm_bwd_f32")
+        return dhB, dhW, dscale, doffset, None, None, None
+
+
+class IndexRowsFn(torch.autograd.Function):
+    """x[idx] for UNIQUE row indices (sampled_nodes: positions of the previous layer's nodes
+    among the sampled ones, sampler.py:143). Forward: HIP row gather (reads strided rows in
+    place). Backward: zeros + one HIP row scatter — no index sort, which torch's generic
+    index backward needs because it must allow repeated indices."""
+
+    @staticmethod
+    def forward(ctx, x, idx):
+        from . import custom_sparse_ops as cso
+
+        out = torch.empty((idx.numel(), x.shape[1]), dtype=x.dtype, device=x.device)
+        cso.gather_rows(x, idx, out, None, n=idx.numel())
+        ctx.save_for_backward(idx)
+        ctx.n = x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import custom_sparse_ops as cso
+
+        (idx,) = ctx.saved_tensors
+        gx = torch.zeros((ctx.n, g.shape[1]), dtype=g.dtype, device=g.device)
+        cso.gather_rows(g.contiguous(), None, gx, idx, n=idx.numel())
+        return gx, None
+
+
+def index_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    if idx.dtype != torch.int64 or not idx.is_contiguous():
+        idx = idx.long().contiguous()
+    return IndexRowsFn.apply(x, idx)
+
+
+def sage_norm(hB: Optional[torch.Tensor], hW: torch.Tensor, scale: torch.Tensor, offset: torch.Tensor,
+              p: float = 0.0, training: bool = False) -> torch.Tensor:
+    seed = int(torch.randint(0, 2**62, (1,)).item()) if (training and p > 0) else 0
+    return SageNormFn.apply(hB, hW, scale, offset, float(p), bool(training and p > 0), seed)

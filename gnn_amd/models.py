@@ -6,6 +6,9 @@ so a seeded torch RNG yields the same initial weights). The aggregation is
 (rocBLAS/hipBLASLt GEMMs, elementwise) and is not part of the hand-written HIP path.
 
 ``spmm_fn`` lets the CPU baseline (oracle/) run the same modules with torch.sparse.mm.
+``fused=True`` (GPU training) runs each layer's elementwise tail — ELU, row standardise,
+scale/offset and the following dropout — as one HIP kernel (gnn_amd.fused.sage_norm)
+instead of ~15 torch kernels; the math is the same (tests/test_fused_gpu.py).
 """
 from __future__ import annotations
 
@@ -45,13 +48,23 @@ class GraphSageConvolution(nn.Module):
         var = out.var(dim=1, unbiased=False).view(out.shape[0], 1) + 1e-9
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
+    def forward_fused(self, x, adj, sampled_nodes, p, training):
+        from .fused import index_rows, sage_norm
+
+        if self.order > 0:
+            feat = self.spmm_fn(adj, x)
+            xs = index_rows(x, sampled_nodes)
+            return sage_norm(self.linearB(xs), self.linearW(feat), self.scale, self.offset, p, training)
+        return sage_norm(None, self.linearW(x), self.scale, self.offset, p, training)
+
 
 class GraphSage(nn.Module):
     """models.py:27-44."""
 
-    def __init__(self, nfeat, nhid, orders, dropout, spmm_fn=None):
+    def __init__(self, nfeat, nhid, orders, dropout, spmm_fn=None, fused=False):
         super().__init__()
         layers = len(orders)
+        self.fused = fused
         self.nhid = (1 + orders[-1]) * nhid
         self.gcs = nn.ModuleList()
         self.gcs.append(GraphSageConvolution(nfeat, nhid, orders[0], spmm_fn=spmm_fn))
@@ -61,7 +74,10 @@ class GraphSage(nn.Module):
 
     def forward(self, x, adjs, sampled_nodes):
         for idx in range(len(self.gcs)):
-            x = self.dropout(self.gcs[idx](x, adjs[idx], sampled_nodes[idx]))
+            if self.fused:
+                x = self.gcs[idx].forward_fused(x, adjs[idx], sampled_nodes[idx], self.dropout.p, self.training)
+            else:
+                x = self.dropout(self.gcs[idx](x, adjs[idx], sampled_nodes[idx]))
         return x
 
 
@@ -87,13 +103,20 @@ class GraphConvolution(nn.Module):
         var = out.var(dim=1, unbiased=False).view(out.shape[0], 1) + 1e-9
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
+    def forward_fused(self, x, adj, p, training):
+        from .fused import sage_norm
+
+        feat = self.spmm_fn(adj, x) if self.order > 0 else x
+        return sage_norm(None, self.linear(feat), self.scale, self.offset, p, training)
+
 
 class GCN(nn.Module):
     """models.py:67-83."""
 
-    def __init__(self, nfeat, nhid, orders, dropout, spmm_fn=None):
+    def __init__(self, nfeat, nhid, orders, dropout, spmm_fn=None, fused=False):
         super().__init__()
         layers = len(orders)
+        self.fused = fused
         self.nhid = nhid
         self.gcs = nn.ModuleList()
         self.gcs.append(GraphConvolution(nfeat, nhid, orders[0], spmm_fn=spmm_fn))
@@ -103,7 +126,10 @@ class GCN(nn.Module):
 
     def forward(self, x, adjs, sampled_nodes):
         for idx in range(len(self.gcs)):
-            x = self.dropout(self.gcs[idx](x, adjs[idx]))
+            if self.fused:
+                x = self.gcs[idx].forward_fused(x, adjs[idx], self.dropout.p, self.training)
+            else:
+                x = self.dropout(self.gcs[idx](x, adjs[idx]))
         return x
 
 
@@ -135,12 +161,13 @@ def loss(preds, labels, sigmoid_loss, device):
     return (norm_loss * _ls).sum()
 
 
-def build_model(name: str, nfeat: int, nhid: int, orders, num_classes: int, dropout: float = 0.1, spmm_fn=None):
+def build_model(name: str, nfeat: int, nhid: int, orders, num_classes: int, dropout: float = 0.1, spmm_fn=None,
+                fused: bool = False):
     """main.py:91-97."""
     if name == "graphsage":
-        enc = GraphSage(nfeat=nfeat, nhid=nhid, orders=orders, dropout=dropout, spmm_fn=spmm_fn)
+        enc = GraphSage(nfeat=nfeat, nhid=nhid, orders=orders, dropout=dropout, spmm_fn=spmm_fn, fused=fused)
     elif name == "gcn":
-        enc = GCN(nfeat=nfeat, nhid=nhid, orders=orders, dropout=dropout, spmm_fn=spmm_fn)
+        enc = GCN(nfeat=nfeat, nhid=nhid, orders=orders, dropout=dropout, spmm_fn=spmm_fn, fused=fused)
     else:
         raise ValueError(f"unknown model {name!r} (graphsage/gcn)")
     return GNN(encoder=enc, num_classes=num_classes, dropout=dropout, inp=nfeat)

@@ -4,17 +4,19 @@ Reference: per-rank threads in one process; grads flattened with torch.cat, publ
 shared list, ``threading.Barrier``, summed with P2P ``.to(device)`` copies (main.py:149-168);
 per-rank clip_grad_norm_(5) BEFORE the sum and no averaging (main.py:146,159).
 
-Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). The
-gradients live in ONE flat fp32 buffer from the start (every ``param.grad`` is a view of it),
-so the exchange is a single in-place ``all_reduce(SUM)`` — no cat/split copies — after the
-same per-rank clip. Initial weights are broadcast from rank 0 (the reference never syncs
-them: quirk F in SURVEY.md Appendix B).
+Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). After
+the per-rank clip, the gradients are packed into one flat fp32 buffer (a single copy
+kernel), summed with ONE in-place ``all_reduce(SUM)``, and handed back to the parameters as
+views of that buffer (no copy back). Gradients are reset to None each step, so autograd
+hands its freshly computed tensors over instead of accumulating into old ones. Initial
+weights are broadcast from rank 0 (the reference never syncs them: SURVEY.md Appendix B, F).
 """
 from __future__ import annotations
 
 from typing import Optional
 
 import torch
+from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
 
 from .models import loss as loss_fn
 
@@ -28,41 +30,44 @@ class Trainer:
         self.clip = clip
         self.group = group
         self.params = [p for p in model.parameters() if p.requires_grad]
-        n = sum(p.numel() for p in self.params)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=self.device)
-        off = 0
-        for p in self.params:
-            p.grad = self.flat_grad[off: off + p.numel()].view_as(p)
-            off += p.numel()
         self.optimizer = torch.optim.Adam(self.params, lr=lr)
         self.world = 1
-        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+        if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world = torch.distributed.get_world_size(group)
         if self.world > 1:
             self.broadcast_parameters()
 
     @property
     def num_params(self) -> int:
-        return self.flat_grad.numel()
+        return sum(p.numel() for p in self.params)
 
     def broadcast_parameters(self):
-        flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+        flat = _flatten_dense_tensors([p.detach() for p in self.params])
         torch.distributed.broadcast(flat, src=0, group=self.group)
-        off = 0
         with torch.no_grad():
-            for p in self.params:
-                p.copy_(flat[off: off + p.numel()].view_as(p))
-                off += p.numel()
+            for p, v in zip(self.params, _unflatten_dense_tensors(flat, self.params)):
+                p.copy_(v)
 
-    def step(self, x0, adjs, sampled_nodes, labels, exchange: bool = True) -> torch.Tensor:
-        self.flat_grad.zero_()
+    def allreduce_grads(self) -> Optional[torch.Tensor]:
+        """Σ over ranks of the (already clipped) gradients, in one flat buffer."""
+        if self.world <= 1:
+            return None
+        grads = [p.grad for p in self.params]
+        flat = _flatten_dense_tensors(grads)
+        torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
+        for p, g in zip(self.params, _unflatten_dense_tensors(flat, grads)):
+            p.grad = g
+        return flat
+
+    def step(self, x0, adjs, sampled_nodes, labels) -> torch.Tensor:
+        for p in self.params:
+            p.grad = None
         self.model.train()
         out = self.model(x0, adjs, sampled_nodes)
         loss = loss_fn(out, labels, self.sigmoid_loss, self.device)
         loss.backward()
         torch.nn.utils.clip_grad_norm_(self.params, self.clip)
-        if exchange and self.world > 1:
-            torch.distributed.all_reduce(self.flat_grad, op=torch.distributed.ReduceOp.SUM, group=self.group)
+        self.allreduce_grads()
         self.optimizer.step()
         return loss.detach()
 

@@ -18,13 +18,21 @@ from gnn_amd import custom_sparse_ops as cso  # noqa: E402
 
 
 def time_call(op, X, unit, reps):
+    """(median main-kernel ms, bytes, median whole-call ms incl. the combine pass)."""
     cso.enable_timing(True)
+    tot = []
     for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         cso.spmm_csr(op, X, unit_nnz=unit)
+        e1.record()
+        tot.append((e0, e1))
+    torch.cuda.synchronize()
     recs = cso.take_timing_records()
     cso.enable_timing(False)
     ms = np.array([r[1] for r in recs])
-    return float(np.median(ms)), recs[0][2]
+    tms =np.array([a.elapsed_time(b) for a, b in tot])
+    return float(np.median(ms)), recs[0][2], float(np.median(tms))
 
 
 def main():
@@ -49,11 +57,12 @@ def main():
                 X = torch.randn(o.shape[1], F, device=dev)
                 for unit in [int(u) for u in args.units.split(",")]:
                     cso.spmm_csr(o, X, unit_nnz=unit)  # warm
-                    ms, nbytes = time_call(o, X, unit, args.reps)
+                    ms, nbytes, tms = time_call(o, X, unit, args.reps)
                     cfg = cso.spmm_config(o.shape[0], o.nnz, F, unit_nnz=unit)
                     row = dict(layer=li, site=tag, M=o.shape[0], K=o.shape[1], nnz=o.nnz, F=F, unit=cfg["unit_nnz"],
                                units=cfg["units"], vw=cfg["vw"], g=cfg["g"], nj=cfg["nj"], us=round(ms * 1e3, 1),
-                               GBps=round(nbytes / (ms * 1e-3) / 1e9, 1))
+                               GBps=round(nbytes / (ms * 1e-3) / 1e9, 1), call_us=round(tms * 1e3, 1),
+                               call_GBps=round(nbytes / (tms * 1e-3) / 1e9, 1))
                     res.append(row)
                     print(json.dumps(row), flush=True)
         # operand build + transpose costs

@@ -12,8 +12,10 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _declared():
-    with open(os.path.join(REPO, "include", "gnn_spmm.h")) as f:
-        txt = f.read()
+    txt = ""
+    for h in ("gnn_spmm.h", "gnn_layers.h"):
+        with open(os.path.join(REPO, "include", h)) as f:
+            txt += f.read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(gnn_[a-z0-9_]+)\s*\(", txt)))
 

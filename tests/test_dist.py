@@ -55,13 +55,13 @@ def _trainer_worker(rank, world, port, q):
         ref_grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
     ref = sum(ref_grads)
     # the same through the Trainer (model forward signature differs: call pieces directly)
-    tr.flat_grad.zero_()
     out = model(xs[rank])
     loss = torch.nn.BCEWithLogitsLoss(weight=torch.full((4, 1), 0.25), reduction="sum")(out, ys[rank])
     loss.backward()
     torch.nn.utils.clip_grad_norm_(tr.params, 5)
-    dist.all_reduce(tr.flat_grad)
-    q.put((rank, torch.allclose(tr.flat_grad, ref, rtol=1e-6, atol=1e-7),
+    flat = tr.allreduce_grads()
+    got = torch.cat([p.grad.reshape(-1) for p in tr.params])
+    q.put((rank, torch.allclose(flat, ref, rtol=1e-6, atol=1e-7) and torch.allclose(got, ref, rtol=1e-6, atol=1e-7),
            [p.detach().numpy().copy() for p in model.parameters()]))
     dist.destroy_process_group()
 

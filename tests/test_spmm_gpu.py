@@ -207,6 +207,25 @@ def test_transpose_long_columns(dev):
     assert np.array_equal(t.val.cpu().numpy(), trv)
 
 
+@pytest.mark.parametrize("K", [1, 7, 32 * 1024, 32 * 1024 + 1, 60000])
+def test_transpose_k_paths(dev, K):
+    """Tiled counting transpose (K <= 32768, histograms in LDS) and the large-K fallback
+    (atomic slot claim + segmented sort) both give the canonical transpose."""
+    M = 2500
+    rng = np.random.default_rng(K)
+    lens = powerlaw_lens(M, 30, 1.5, rng, min(K, 3000))
+    lens[:3] = min(K, 2000)
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K)
+    t = op.transpose()
+    torch.cuda.synchronize()
+    assert np.array_equal(t.rowptr.cpu().numpy(), trp)
+    assert np.array_equal(t.col.cpu().numpy(), trc)
+    assert np.array_equal(t.val.cpu().numpy(), trv)
+
+
 @pytest.mark.parametrize("F", [26, 100, 602, 1024])
 def test_autograd_backward(dev, F):
     M, K = 700, 900
