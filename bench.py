@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic child run")
     ap.add_argument("--unfused", action="store_true", help="torch elementwise layer tail instead of the HIP one")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     return ap.parse_args()
@@ -70,6 +71,71 @@ def sample_batches(args, lap, labels, train, pl, rank, world):
                                               [1, 1, 1], pl.device_id_of_nodes_group[rank],
                                               pl.idx_of_nodes_on_device_group[rank], None, 1.0, list(range(world))))
     return out
+
+
+def _counter_rows(d):
+    import csv
+    import glob
+
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows.extend(csv.DictReader(fh))
+    return rows
+
+
+def pmc_traffic(hb, F, workdir="/tmp/gnn_bench_pmc"):
+    """HBM-side bytes per launch of the layer-0 forward aggregation kernel from rocprofv3 PMC
+    counters (FETCH_SIZE and WRITE_SIZE in separate passes), corrected by calibrating each
+    counter on a row gather of known bytes with the same row and vector width
+    (MI355X_MICROARCH.md §HBM). Runs the probe as a CHILD process before this process has
+    touched the GPU. Returns a dict, or None if the profiler is unavailable."""
+    import shutil
+    import subprocess
+
+    if shutil.which("rocprofv3") is None:
+        return None
+    os.makedirs(workdir, exist_ok=True)
+    npz = os.path.join(workdir, "batch0.npz")
+    L0 = hb.layers
+    np.savez(npz, **{f"l{i}_{k}": getattr(L, k) for i, L in enumerate(L0)
+                     for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
+             **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
+    probe = os.path.join(REPO, "scripts", "pmc_probe.py")
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(workdir, counter)
+        shutil.rmtree(d, ignore_errors=True)
+        cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
+               sys.executable, probe, npz, "--feat", str(F)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            log(f"pmc pass {counter} failed rc={r.returncode}: {r.stderr[-500:]}")
+            return None
+        calib, spmm = [], []
+        for row in _counter_rows(d):
+            if row.get("Counter_Name") != counter:
+                continue
+            name, v = row.get("Kernel_Name", ""), float(row.get("Counter_Value", "nan"))
+            if "gather_rows_kernel" in name:
+                calib.append(v)
+            elif "spmm_unit_kernel" in name:
+                spmm.append(v)
+        if not calib or not spmm:
+            return None
+        vals[counter] = (float(np.median(calib)), float(np.median(spmm)))
+    n = int(1.2e9 // (F * 4))
+    known = n * F * 4  # bytes read (and written) by one calibration gather
+    fc, fs = vals["FETCH_SIZE"]
+    wc, ws = vals["WRITE_SIZE"]
+    read_corr = known / (fc * 1024.0)
+    write_corr = known / (wc * 1024.0)
+    read_b = fs * 1024.0 * read_corr
+    write_b = ws * 1024.0 * write_corr
+    return {"bytes_per_launch": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
+            "fetch_size_kb_raw": fs, "write_size_kb_raw": ws, "read_correction": round(read_corr, 4),
+            "write_correction": round(write_corr, 4)}
 
 
 def cpu_baseline(args, hb, feats, num_classes):
@@ -98,7 +164,6 @@ def main():
     rank, world, local = init_distributed()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
 
     t0 = time.time()
     spec = graphs.REDDIT if args.graph == "reddit" else graphs.TINY
@@ -112,6 +177,15 @@ def main():
     log(f"placement k={k} per GPU ({time.time() - t0:.1f}s)")
     host_batches = sample_batches(args, lap, labels, train, pl, rank, world)
     log(f"sampled {len(host_batches)} batches ({time.time() - t0:.1f}s); nnz/batch={host_batches[0].nnz()}")
+    traffic = None
+    if rank == 0 and world == 1 and not args.no_traffic:
+        # before this process initialises the GPU: the probe is a child process
+        try:
+            traffic = pmc_traffic(host_batches[0], feats.shape[1])
+        except Exception as e:  # profiler trouble must not sink the benchmark
+            log(f"pmc traffic measurement skipped: {e!r}")
+        log(f"pmc traffic done ({time.time() - t0:.1f}s): {traffic}")
+    torch.cuda.set_device(dev)
 
     store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank)
     exchange = staging.PeerExchange() if world > 1 else None
@@ -167,12 +241,6 @@ def main():
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
     # ---------------------------------------------------------------- roofline
-    by = {}
-    for tag, ms, nbytes in recs:
-        e = by.setdefault(tag, [0.0, 0, 0])
-        e[0] += ms
-        e[1] += nbytes
-        e[2] += 1
     roof = None
     spmm_detail = {}
     if recs:
@@ -192,10 +260,14 @@ def main():
         ms, nbytes, n = site[dom]
         achieved = nbytes / (ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # GB per launch leaving L2 for the Infinity Cache / HBM (PMC, calibrated)
+                "traffic": round(traffic["bytes_per_launch"] / 1e9, 4) if traffic else None,
                 "kernel": f"spmm_unit_kernel ({'layer-0 forward' if dom == 'fwd0' else dom}), "
                           f"avg {1e3 * ms / n:.1f} us/launch over {n} launches, "
                           f"{nbytes / n / 1e9:.3f} GB algorithmic per launch"}
+        if traffic:
+            roof["traffic_detail"] = traffic
         tot_ms = sum(v[0] for v in site.values())
         tot_b = sum(v[1] for v in site.values())
         roof["all_spmm_GBps"] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)

@@ -268,7 +268,32 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
 // Operand builder: value = (float)((1.0 / full_degree(row)) * (double)normfact[col]),
 // the formula of cuda_spmm.cu:800 evaluated in double. One wave per row.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void cmpx_reg(int& k, float& v, int lane, int mask);
+// Bitonic sort helpers, "all comparators ascending" form: positions >= L act as +inf.
+constexpr int SEG_WAVE_LDS = 512;
+constexpr int SEG_BLOCK_LDS = 16384;
+
+__device__ __forceinline__ void cmpx_reg(int& k, float& v, int lane, int mask) {
+  const int pk = __shfl_xor(k, mask);
+  const float pv = __shfl_xor(v, mask);
+  const bool lower = lane < (lane ^ mask);
+  const bool take = lower ? (pk < k) : (pk > k);
+  if (take) {
+    k = pk;
+    v = pv;
+  }
+}
+
+// Pair p of a bitonic step -> element positions (i < j).
+__device__ __forceinline__ void bitonic_pair(int p, int size, int d, bool flip, int& i, int& j) {
+  if (flip) {
+    const int half = size >> 1;
+    i = (p / half) * size + (p % half);
+    j = i ^ (size - 1);
+  } else {
+    i = (p / d) * (2 * d) + (p % d);
+    j = i + d;
+  }
+}
 
 // Also restores the coalesced (column-ascending) order the reference gets from
 // .coalesce(): rows found unsorted are sorted here when short (<= 64 entries, in
@@ -278,10 +303,12 @@ template <typename CT>
 __global__ __launch_bounds__(256) void build_operand_kernel(
     const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
     const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
-    int* __restrict__ out_col, float* __restrict__ out_val,
-    int* __restrict__ counters, int* __restrict__ list_mid, int* __restrict__ list_long, int block_cap) {
+    int* __restrict__ out_col, float* __restrict__ out_val) {
+  __shared__ int sk[4][SEG_WAVE_LDS];
+  __shared__ float sv[4][SEG_WAVE_LDS];
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + w;
   if (r >= nrows) return;
   const int b = rowptr[r];
   const int e = rowptr[r + 1];
@@ -312,11 +339,56 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
       out_col[b + lane] = k;
       out_val[b + lane] = v;
     }
-  } else if (lane == 0) {
-    if (L <= block_cap) {
-      list_mid[atomicAdd(&counters[0], 1)] = r;
-    } else {
-      list_long[atomicAdd(&counters[1], 1)] = r;
+    return;
+  }
+  // Longer unsorted rows (never produced by scipy slicing, kept for generality): bitonic
+  // sort of (column, value) by this wave, in its LDS region (<= 512) or in place in global
+  // memory (the lanes' own stores are made visible to the wave by a workgroup fence).
+  int n = 1;
+  while (n < L) n <<= 1;
+  if (L <= SEG_WAVE_LDS) {
+    for (int i = lane; i < n; i += 64) {
+      const int c = (i < L) ? (int)colidx[b + i] : INT_MAX;
+      sk[w][i] = c;
+      sv[w][i] = (i < L) ? (float)(inv * (double)normfact[c]) : 0.0f;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int d = size >> 1; d >= 1; d >>= 1) {
+      const bool flip = (d == (size >> 1));
+      for (int p = lane; p < (n >> 1); p += 64) {
+        int i, j;
+        bitonic_pair(p, size, d, flip, i, j);
+        if (L <= SEG_WAVE_LDS) {
+          const int ki = sk[w][i], kj = sk[w][j];
+          if (kj < ki) {
+            const float vi = sv[w][i], vj = sv[w][j];
+            sk[w][i] = kj;
+            sk[w][j] = ki;
+            sv[w][i] = vj;
+            sv[w][j] = vi;
+          }
+        } else if (j < L) {
+          const int ki = out_col[b + i], kj = out_col[b + j];
+          if (kj < ki) {
+            const float vi = out_val[b + i], vj = out_val[b + j];
+            out_col[b + i] = kj;
+            out_col[b + j] = ki;
+            out_val[b + i] = vj;
+            out_val[b + j] = vi;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (L <= SEG_WAVE_LDS) {
+    for (int i = lane; i < L; i += 64) {
+      out_col[b + i] = sk[w][i];
+      out_val[b + i] = sv[w][i];
     }
   }
 }
@@ -544,34 +616,9 @@ __global__ __launch_bounds__(256) void tr_tile_scatter_kernel(
 // Bitonic network in its "all comparators ascending" form (first step of every merge
 // compares mirrored positions), so positions >= L can be treated as +inf and skipped.
 // Segments: <=64 in registers, <=512 in a per-wave LDS region, <=16384 by one 1024-thread
-// workgroup in LDS, longer ones by one workgroup in global memory.
+// workgroup in LDS, longer ones by one workgroup in global memory. (Helpers: above the
+// operand builder, which uses the same network.)
 // ---------------------------------------------------------------------------------
-constexpr int SEG_WAVE_LDS = 512;
-constexpr int SEG_BLOCK_LDS = 16384;
-
-__device__ __forceinline__ void cmpx_reg(int& k, float& v, int lane, int mask) {
-  const int pk = __shfl_xor(k, mask);
-  const float pv = __shfl_xor(v, mask);
-  const bool lower = lane < (lane ^ mask);
-  const bool take = lower ? (pk < k) : (pk > k);
-  if (take) {
-    k = pk;
-    v = pv;
-  }
-}
-
-// Pair p of a bitonic step -> element positions (i < j).
-__device__ __forceinline__ void bitonic_pair(int p, int size, int d, bool flip, int& i, int& j) {
-  if (flip) {
-    const int half = size >> 1;
-    i = (p / half) * size + (p % half);
-    j = i ^ (size - 1);
-  } else {
-    i = (p / d) * (2 * d) + (p % d);
-    j = i + d;
-  }
-}
-
 __global__ __launch_bounds__(256) void segsort_wave_kernel(const int* __restrict__ ptr, int nseg,
                                                            int* __restrict__ key, float* __restrict__ val,
                                                            int* __restrict__ counters,
@@ -774,20 +821,20 @@ int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
 }
 
 int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
+  (void)M;
   (void)F;
-  // Units are equal-sized (S nonzeros), so ~4k of them (2 per wave slot of the chip at 8
-  // waves/CU) already balance power-law rows. Bigger units cut fewer rows: a row is split
-  // (and pays a slab round trip + the combine pass) with probability ~ mean_len / S, so S
-  // is kept >= 4 x the mean row length when that still leaves >= 2k units.
-  int64_t s = ceil_div(nnz, 4096);
-  const int64_t mean_len = M > 0 ? ceil_div(nnz, M) : 1;
-  if (s < 4 * mean_len && ceil_div(nnz, 4 * mean_len) >= 2048) s = 4 * mean_len;
+  // Units are equal-sized (S nonzeros), which balances power-law rows by construction.
+  // Measured on the Reddit LADIES layers (scripts/spmm_microbench.py, with L2 column
+  // tiles): S = 256 is the sweet spot between per-row flush/search overhead (small S) and
+  // too few waves per column-tile pass (large S: layer-1 forward 262 us at S = 404 vs
+  // 208 us at 256). Small problems keep >= 2048 units for parallelism, S >= 16.
+  int64_t s = 256;
+  if (ceil_div(nnz, s) < 2048) s = ceil_div(nnz, 2048);
   if (s < 16) s = 16;
-  if (s > 4096) s = 4096;
   return s;
 }
 
-SpmmCfg make_cfg(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
                  const void* Y, int64_t unit) {
   SpmmCfg c{};
   c.vw = pick_vw(F, ldx, ldy, X, Y);
@@ -805,6 +852,35 @@ SpmmCfg make_cfg(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, co
       c.g = g;
       c.nj = (int)nj;
       c.tiles = (int)tiles;
+    }
+  }
+  // L2-sized column tiles. Each XCD's 4 MiB L2 sees random rows of X; when X rows are
+  // re-read many times (nnz/K >= 8) cut the columns into tiles whose slice of X
+  // (K rows x tile width) is about one L2, processed tile after tile (grid.y is the slow
+  // dispatch dimension), so re-reads hit L2 instead of the Infinity Cache. Measured on the
+  // Reddit LADIES layers: 1.3-1.9x.
+  if (K > 0 && nnz >= 8 * K) {
+    const double target_cols = (4.0 * 1024 * 1024 / 4.0) / (double)K;  // floats per row slice
+    int64_t cols = (int64_t)c.vw * 16;                                    // smallest: G=16, NJ=1
+    while (cols * 2 <= F && (double)(cols * 2) <= target_cols * 1.41421356) cols *= 2;
+    if (cols < F) {
+      const int64_t per = cols / c.vw;  // lanes x chunks
+      c.g = per >= 64 ? 64 : (int)per;
+      c.nj = per >= 64 ? (int)(per / 64) : 1;
+      if (c.nj > 8) c.nj = 8;
+      c.tiles = (int)ceil_div(F, (int64_t)c.vw * c.g * c.nj);
+    }
+  }
+  // Experiment override (benchmarks only): GNN_SPMM_G / GNN_SPMM_NJ force the lane group
+  // and column chunks; F is then covered by ceil(F / (VW*G*NJ)) column tiles (grid.y).
+  if (const char* eg = getenv("GNN_SPMM_G")) {
+    const int g = atoi(eg);
+    const char* en = getenv("GNN_SPMM_NJ");
+    const int nj = en ? atoi(en) : 1;
+    if ((g == 16 || g == 32 || g == 64) && nj >= 1 && nj <= 8) {
+      c.g = g;
+      c.nj = nj;
+      c.tiles = (int)ceil_div(F, (int64_t)c.vw * g * nj);
     }
   }
   c.unit = unit > 0 ? unit : default_unit(M, nnz, F);
@@ -914,14 +990,14 @@ const char* gnn_version(void) { return "gnn_spmm gfx950 " GNN_BUILD_ID; }
 int64_t gnn_spmm_default_unit_nnz(int64_t M, int64_t nnz, int64_t F) { return default_unit(M, nnz, F); }
 
 size_t gnn_spmm_workspace_bytes(int64_t M, int64_t nnz, int64_t F, int64_t unit_nnz) {
-  const SpmmCfg c = make_cfg(M, nnz, F, F, F, nullptr, nullptr, unit_nnz);
+  const SpmmCfg c = make_cfg(M, 0, nnz, F, F, F, nullptr, nullptr, unit_nnz);
   return align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
 }
 
-int gnn_spmm_config(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y,
-                    int64_t unit_nnz, int32_t out[6]) {
+int gnn_spmm_config(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+                    const void* Y, int64_t unit_nnz, int32_t out[6]) {
   GNN_REQUIRE(out != nullptr, "gnn_spmm_config: out is NULL");
-  const SpmmCfg c = make_cfg(M, nnz, F, ldx, ldy, X, Y, unit_nnz);
+  const SpmmCfg c = make_cfg(M, K, nnz, F, ldx, ldy, X, Y, unit_nnz);
   out[0] = c.vw;
   out[1] = c.g;
   out[2] = c.nj;
@@ -948,7 +1024,7 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
   if (M == 0 || F == 0) return 0;
   GNN_REQUIRE(rowptr && Y, "gnn_spmm_csr_f32: NULL rowptr/Y");
   GNN_REQUIRE(nnz == 0 || (col && val && X), "gnn_spmm_csr_f32: NULL col/val/X");
-  const SpmmCfg c = make_cfg(M, nnz, F, ldx, ldy, X, Y, unit_nnz);
+  const SpmmCfg c = make_cfg(M, K, nnz, F, ldx, ldy, X, Y, unit_nnz);
   GNN_REQUIRE(c.nunits * c.unit < (int64_t)INT_MAX + c.unit, "gnn_spmm_csr_f32: unit overflow");
   GNN_REQUIRE(c.nunits <= (int64_t)INT_MAX / 2, "gnn_spmm_csr_f32: too many units");
   const size_t need = align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
@@ -996,31 +1072,25 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
               "gnn_build_operand_f32: colidx_bytes must be 2, 4 or 8 (got %d)", colidx_bytes);
   if (nrows == 0 || nnz == 0) return 0;
   GNN_REQUIRE(fullrowptr && rowptr && colidx && normfact && csr_col && csr_val, "gnn_build_operand_f32: NULL input");
-  GNN_REQUIRE(workspace && workspace_bytes >= segsort_ws(nrows), "gnn_build_operand_f32: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)ceil_div(nrows, 4));
-  const SegLists l = seg_lists(workspace, nrows);
-  GNN_HIP(hipMemsetAsync(l.counters, 0, 16, st), "operand sort-list counters memset");
+  (void)workspace;  // rows are sorted in the build kernel itself; kept for ABI stability
+  (void)workspace_bytes;
   switch (colidx_bytes) {
     case 2:
       build_operand_kernel<int16_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
-                                                                l.list_long, SEG_BLOCK_LDS);
+                                                                (int)nrows, csr_col, csr_val);
       break;
     case 4:
       build_operand_kernel<int32_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
-                                                                l.list_long, SEG_BLOCK_LDS);
+                                                                (int)nrows, csr_col, csr_val);
       break;
     default:
       build_operand_kernel<int64_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val, l.counters, l.list_mid,
-                                                                l.list_long, SEG_BLOCK_LDS);
+                                                                (int)nrows, csr_col, csr_val);
       break;
   }
   GNN_LAUNCHED("build_operand_kernel");
-  int rc = run_list_sorters(rowptr, csr_col, csr_val, l, st);
-  if (rc) return rc;
   if (coo_indices) {
     csr_to_coo_indices_kernel<<<grid, dim3(256), 0, st>>>(rowptr, csr_col, (int)nrows, nnz, coo_indices);
     GNN_LAUNCHED("csr_to_coo_indices_kernel");

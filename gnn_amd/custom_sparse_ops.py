@@ -176,12 +176,21 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
     F = dense.shape[1]
     ldx = dense.stride(0) if dense.shape[0] > 1 else max(F, 1)
     dev = dense.device
+    # Padded rows (the layer-0 staging buffer: 602 floats in 604-float rows): let the
+    # kernel run over the padded width Fk = round_up(F, 4) so it can use 16-byte loads, into
+    # an output with the same padded stride; the caller gets the (M x F) view.
+    Fk = F
+    if F % 4 and ldx % 4 == 0 and dense.data_ptr() % 16 == 0:
+        F4 = F + (4 - F % 4)
+        avail = dense.untyped_storage().nbytes() // 4 - dense.storage_offset()
+        if ldx >= F4 and (K - 1) * ldx + F4 <= avail:
+            Fk = F4
     with torch.cuda.device(dev):
-        out = torch.empty((M, F), dtype=torch.float32, device=dev)
+        out = torch.empty((M, Fk), dtype=torch.float32, device=dev)
         if M == 0 or F == 0:
-            return out
+            return out[:, :F]
         L = _lib.lib()
-        wsb = L.gnn_spmm_workspace_bytes(M, op.nnz, F, unit_nnz)
+        wsb = L.gnn_spmm_workspace_bytes(M, op.nnz, Fk, unit_nnz)
         ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
         st = _stream(dev)
         if _timing_enabled:
@@ -192,9 +201,9 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
             L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
             _timing_records.append((tag, e0, e1, algorithmic_bytes(M, op.nnz, F)))
         _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
-                                      dense.data_ptr(), ldx, out.data_ptr(), F, F,
+                                      dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
                                       ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32")
-    return out
+    return out if Fk == F else out[:, :F]
 
 
 class SparseDenseMM(torch.autograd.Function):
@@ -232,10 +241,6 @@ def spmm_load_balance(sparseMat, denseMat) -> torch.Tensor:
 spmm_naive = spmm_load_balance
 
 
-def _seg_ws(nrows: int, dev) -> Tuple[torch.Tensor, int]:
-    wsb = _lib.lib().gnn_segsort_workspace_bytes(nrows)
-    return torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev), wsb
-
 
 def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.Tensor, normfact: torch.Tensor,
                   nrows: int, ncols: int, with_coo: bool = True):
@@ -255,10 +260,9 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
         col32 = torch.empty(nnz, dtype=torch.int32, device=dev)
         val = torch.empty(nnz, dtype=torch.float32, device=dev)
         coo = torch.empty((2, nnz), dtype=torch.int64, device=dev) if with_coo else None
-        ws, wsb = _seg_ws(nrows, dev)
         _lib.check(_lib.lib().gnn_build_operand_f32(
             _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
-            nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _ptr(ws), wsb, _stream(dev)),
+            nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), None, 0, _stream(dev)),
             "gnn_build_operand_f32")
     return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
 
@@ -295,8 +299,9 @@ def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.T
 
 
 def spmm_config(M: int, nnz: int, F: int, ldx: Optional[int] = None, ldy: Optional[int] = None,
-                unit_nnz: int = 0) -> dict:
+                unit_nnz: int = 0, K: int = 0) -> dict:
     """Kernel configuration the library picks for a call shape (16-byte aligned buffers)."""
     out = (ctypes.c_int32 * 6)()
-    _lib.check(_lib.lib().gnn_spmm_config(M, nnz, F, ldx or F, ldy or F, 256, 256, unit_nnz, out), "gnn_spmm_config")
+    _lib.check(_lib.lib().gnn_spmm_config(M, K, nnz, F, ldx or F, ldy or F, 256, 256, unit_nnz, out),
+               "gnn_spmm_config")
     return dict(vw=out[0], g=out[1], nj=out[2], tiles=out[3], unit_nnz=out[4], units=out[5])

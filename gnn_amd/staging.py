@@ -50,11 +50,11 @@ class FeatureStore:
         self.gpu_buffer = buf.to(self.device)  # (k x ld), row i = node buffer_nodes[i]
 
     def host_rows_pinned(self, node_ids: np.ndarray) -> torch.Tensor:
-        """Host gather of non-buffered rows into a pinned (n x F) tensor."""
+        """Host gather of non-buffered rows into a pinned (n x ld) tensor (zero padding)."""
         n = len(node_ids)
-        out = torch.empty((n, self.F), dtype=torch.float32).pin_memory()
+        out = torch.zeros((n, self.ld), dtype=torch.float32).pin_memory()
         if n:
-            torch.index_select(self.host, 0, torch.from_numpy(np.asarray(node_ids, dtype=np.int64)), out=out)
+            out[:, : self.F] = self.host[torch.from_numpy(np.asarray(node_ids, dtype=np.int64))]
         return out
 
 
@@ -65,7 +65,7 @@ class StagePlan:
     own_pos: np.ndarray      # X0 rows filled from this rank's buffer
     own_src: np.ndarray      # their slots in the buffer
     host_pos: np.ndarray     # X0 rows filled from host memory
-    host_rows: torch.Tensor  # pinned (n_host x F) rows, already gathered on the host
+    host_rows: torch.Tensor  # pinned (n_host x ld) rows, already gathered on the host
     peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
     pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos)
@@ -110,7 +110,7 @@ class Stager:
             host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
             if len(plan.host_pos):
-                cso.gather_rows(host_dev, None, x0[:, : self.store.F], host_pos, n=len(plan.host_pos))
+                cso.gather_rows(host_dev, None, x0, host_pos, n=len(plan.host_pos))
             if self.exchange is not None:
                 self.exchange.exchange(plan, x0, self.store)
             ev = torch.cuda.Event()

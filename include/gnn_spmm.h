@@ -60,7 +60,7 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
 
 /* Describe the kernel configuration gnn_spmm_csr_f32 would pick (vector width, lanes per
  * column group, column chunks per lane, column tiles, units). For diagnostics/benchmarks. */
-int gnn_spmm_config(int64_t M, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,
+int gnn_spmm_config(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,
                     const void* X, const void* Y, int64_t unit_nnz, int32_t out[6]);
 
 /* Optional timing hook: when set, the NEXT gnn_spmm_csr_f32 call on this thread records
@@ -83,7 +83,8 @@ void gnn_spmm_set_timing_events(void* start, void* stop);
  * (cuda_spmm.cu:825); rows are assumed free of duplicate columns (scipy slicing output).
  * Outputs: csr_col (int32, nnz), csr_val (fp32, nnz) and, if coo_indices != NULL, the
  * coalesced COO indices int64[2][nnz] (row-major: all rows then all columns).
- * `workspace` >= gnn_segsort_workspace_bytes(nrows) bytes.
+ * `workspace` is not used any more (rows are sorted inside the build kernel) and may be
+ * NULL; the parameter is kept for ABI stability.
  * ------------------------------------------------------------------------------- */
 size_t gnn_segsort_workspace_bytes(int64_t nseg);
 int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr,

@@ -58,7 +58,7 @@ def main():
                 for unit in [int(u) for u in args.units.split(",")]:
                     cso.spmm_csr(o, X, unit_nnz=unit)  # warm
                     ms, nbytes, tms = time_call(o, X, unit, args.reps)
-                    cfg = cso.spmm_config(o.shape[0], o.nnz, F, unit_nnz=unit)
+                    cfg = cso.spmm_config(o.shape[0], o.nnz, F, unit_nnz=unit, K=o.shape[1])
                     row = dict(layer=li, site=tag, M=o.shape[0], K=o.shape[1], nnz=o.nnz, F=F, unit=cfg["unit_nnz"],
                                units=cfg["units"], vw=cfg["vw"], g=cfg["g"], nj=cfg["nj"], us=round(ms * 1e3, 1),
                                GBps=round(nbytes / (ms * 1e-3) / 1e9, 1), call_us=round(tms * 1e3, 1),

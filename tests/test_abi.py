@@ -65,6 +65,15 @@ def test_workspace_and_config():
     assert c["vw"] == 2  # F itself is not a multiple of 4
     c = spmm_config(100, 1000, 5000)
     assert c["tiles"] >= 2 and c["nj"] <= 8
+    # L2-sized column tiles when X rows are re-read (nnz >= 8 K): slice of X ~ 4 MiB
+    c = spmm_config(8680, 868338, 1024, K=15768)  # layer-1 forward: 64-float slices
+    assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 16, 1, 16)
+    c = spmm_config(15768, 868338, 1024, K=8680)  # layer-1 backward: 128-float slices
+    assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 32, 1, 8)
+    c = spmm_config(15768, 1821171, 604, K=22153, ldx=604, ldy=604)  # layer 0, padded rows
+    assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 16, 1, 10)
+    c = spmm_config(512, 14876, 1024, K=8680)  # little reuse: one tile
+    assert c["tiles"] == 1
     assert L.gnn_csr_transpose_workspace_bytes(10, 1000, 50) >= 4000
     assert L.gnn_segsort_workspace_bytes(100) >= 800
 
