@@ -29,7 +29,9 @@ _SIGNATURES = {
     "gnn_spmm_default_unit_nnz": (_I64, [_I64, _I64, _I64]),
     "gnn_spmm_workspace_bytes": (_SZ, [_I64, _I64, _I64, _I64]),
     "gnn_spmm_csr_f32": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _SZ, _I64, _VP]),
-    "gnn_spmm_config": (_INT, [_I64, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_int32)]),
+    "gnn_spmm_csr_f32_ex": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _I64, _VP,
+                                   _VP, _SZ, _I64, _VP]),
+    "gnn_spmm_config":(_INT, [_I64, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gnn_spmm_set_timing_events": (None, [_VP, _VP]),
     "gnn_segsort_workspace_bytes": (_SZ, [_I64]),
     "gnn_build_operand_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
@@ -38,11 +40,12 @@ _SIGNATURES = {
     "gnn_csr_transpose": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
     "gnn_gather_rows_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
     # include/gnn_layers.h
-    "gnn_sage_norm_fwd_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _I64, ctypes.c_float,
+    "gnn_sage_norm_fwd_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _I64, ctypes.c_float,
                                      ctypes.c_uint64, _INT, _VP, _I64, _VP, _VP, _VP]),
     "gnn_sage_norm_bwd_workspace_bytes": (_SZ, [_I64, _I64]),
-    "gnn_sage_norm_bwd_f32": (_INT, [_VP, _I64, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _I64,
-                                     ctypes.c_float, ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "gnn_sage_norm_bwd_f32": (_INT, [_VP, _I64, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64,
+                                     ctypes.c_float, ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ,
+                                     _VP]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)

@@ -1,15 +1,16 @@
 // sage.hip — fused GraphSAGE / GCN layer epilogue (forward + backward), gfx950.
 //
 // Reference (models.py:16-25, 58-64, 43, 82): after the two linear layers, torch runs
-// cat -> elu -> mean -> var -> sub -> mul(scale) -> rsqrt -> mul -> add(offset) -> dropout,
-// each a separate pass over the (M x 1024) activation, and about twice as many passes in
-// backward. Here one wave owns one row: the row (<= 2048 floats, <= 8 float4 per lane) is
-// read once into registers, ELU'd, reduced twice with wave shuffles (mean, then the centred
+// bias-add -> cat -> elu -> mean -> var -> sub -> mul(scale) -> rsqrt -> mul -> add(offset) ->
+// dropout, each a separate pass over the (M x 1024) activation, and about twice as many
+// passes in backward (plus one column-sum kernel per linear bias). Here one wave owns one
+// row: the row (<= 2048 floats, <= 8 float4 per lane) is read once into registers, the
+// linear biases added, ELU'd, reduced twice with wave shuffles (mean, then the centred
 // second moment: the same two-pass variance torch computes), normalised, scaled, dropped
-// out and stored once. Backward re-reads the linear outputs and the saved per-row mean and
-// rstd, regenerates the dropout mask from its counter hash, and writes the two input
-// gradients in one pass; d(scale), d(offset) are column sums reduced per workgroup into a
-// slab and then summed over workgroups in a fixed order (deterministic, no atomics).
+// out and stored once. Backward re-reads the bias-free linear outputs and the saved per-row
+// mean and rstd, regenerates the dropout mask from its counter hash, and writes the two
+// input gradients in one pass; d(scale), d(offset) and d(bias) are column sums reduced per
+// workgroup into a slab and then summed over workgroups in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -25,6 +26,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int SN_MAXV = 8;   // float4 per lane: D <= 64 * 4 * 8 = 2048
 constexpr int BWD_MAX_GRID = 512;
+constexpr int NRED = 3;      // column sums: d(scale), d(offset), d(bias)
 
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
@@ -51,15 +53,24 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, float p) 
 __device__ __forceinline__ float elu1(float h) { return h > 0.0f ? h : expm1f(h); }
 __device__ __forceinline__ float elu1_grad(float h) { return h > 0.0f ? 1.0f : expf(h); }
 
-__device__ __forceinline__ f4 load_h(const float* hB, int64_t ldb, int D1, const float* hW, int64_t ldw, int r,
-                                     int c) {
-  return (c < D1) ? *reinterpret_cast<const f4*>(hB + (int64_t)r * ldb + c)
-                  : *reinterpret_cast<const f4*>(hW + (int64_t)r * ldw + (c - D1));
+// Pre-activation of column c of row r: the linear output plus its bias (when given).
+__device__ __forceinline__ f4 load_h(const float* hB, int64_t ldb, const float* bB, int D1, const float* hW,
+                                     int64_t ldw, const float* bW, int r, int c) {
+  if (c < D1) {
+    f4 h = *reinterpret_cast<const f4*>(hB + (int64_t)r * ldb + c);
+    if (bB) h += *reinterpret_cast<const f4*>(bB + c);
+    return h;
+  }
+  f4 h = *reinterpret_cast<const f4*>(hW + (int64_t)r * ldw + (c - D1));
+  if (bW) h += *reinterpret_cast<const f4*>(bW + (c - D1));
+  return h;
 }
 
 template <int NV>
-__global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restrict__ hB, int64_t ldb, int D1,
-                                                            const float* __restrict__ hW, int64_t ldw, int D,
+__global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restrict__ hB, int64_t ldb,
+                                                            const float* __restrict__ bB, int D1,
+                                                            const float* __restrict__ hW, int64_t ldw,
+                                                            const float* __restrict__ bW, int D,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ offset, int M, float p,
                                                             float inv_keep, uint64_t seed, int training,
@@ -74,7 +85,7 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
   for (int k = 0; k < NV; ++k) {
     const int c = (lane + 64 * k) * 4;
     if (c < D) {
-      const f4 h = load_h(hB, ldb, D1, hW, ldw, r, c);
+      const f4 h = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
       o[k] = f4{elu1(h.x), elu1(h.y), elu1(h.z), elu1(h.w)};
       s += (o[k].x + o[k].y) + (o[k].z + o[k].w);
     } else {
@@ -118,18 +129,20 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
 
 template <int NV>
 __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
-    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb, int D1,
-    const float* __restrict__ hW, int64_t ldw, int D, const float* __restrict__ scale,
-    const float* __restrict__ mean, const float* __restrict__ rstd, int M, float p, float inv_keep, uint64_t seed,
-    int training, float* __restrict__ dhB, float* __restrict__ dhW, float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][2][D]
+    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb,
+    const float* __restrict__ bB, int D1, const float* __restrict__ hW, int64_t ldw, const float* __restrict__ bW,
+    int D, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd, int M,
+    float p, float inv_keep, uint64_t seed, int training, float* __restrict__ dhB, float* __restrict__ dhW,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves][D], reused per sum
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  f4 ds[NV], db[NV];
+  f4 ds[NV], db[NV], dbi[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     ds[k] = f4(0.0f);
     db[k] = f4(0.0f);
+    dbi[k] = f4(0.0f);
   }
   for (int r = blockIdx.x * 4 + w; r < M; r += gridDim.x * 4) {
     const float m = mean[r];
@@ -140,7 +153,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
     for (int k = 0; k < NV; ++k) {
       const int c = (lane + 64 * k) * 4;
       if (c < D) {
-        h[k] = load_h(hB, ldb, D1, hW, ldw, r, c);
+        h[k] = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
         const f4 o = f4{elu1(h[k].x), elu1(h[k].y), elu1(h[k].z), elu1(h[k].w)};
         xh[k] = (o - m) * rs;
         f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
@@ -170,6 +183,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
         const f4 dxo = rs * (gx[k] - a - xh[k] * b);
         const f4 dh = f4{dxo.x * elu1_grad(h[k].x), dxo.y * elu1_grad(h[k].y), dxo.z * elu1_grad(h[k].z),
                          dxo.w * elu1_grad(h[k].w)};
+        dbi[k] += dh;
         if (c < D1) {
           *reinterpret_cast<f4*>(dhB + (int64_t)r * D1 + c) = dh;
         } else {
@@ -178,38 +192,37 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
       }
     }
   }
-  // workgroup column sums of d(scale) and d(offset) -> partial[blockIdx.x][2][D]
+  // workgroup column sums -> partial[blockIdx.x][q][D], q = 0 d(scale), 1 d(offset), 2 d(bias)
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int c = (lane + 64 * k) * 4;
-    if (c < D) {
-      *reinterpret_cast<f4*>(red + (w * 2 + 0) * D + c) = ds[k];
-      *reinterpret_cast<f4*>(red + (w * 2 + 1) * D + c) = db[k];
+  for (int q = 0; q < NRED; ++q) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = (lane + 64 * k) * 4;
+      if (c < D) *reinterpret_cast<f4*>(red + w * D + c) = (q == 0) ? ds[k] : (q == 1) ? db[k] : dbi[k];
     }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 2 * D; i += 256) {
-    const int half = i / D, c = i % D;
-    float s = 0.0f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) s += red[(ww * 2 + half) * D + c];
-    partial[(int64_t)blockIdx.x * 2 * D + i] = s;
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) {
+      partial[((int64_t)blockIdx.x * NRED + q) * D + c] = (red[c] + red[D + c]) + (red[2 * D + c] + red[3 * D + c]);
+    }
+    __syncthreads();
   }
 }
 
-// Column sums over the G workgroup partials: a workgroup owns 64 of the 2D columns; its 4
-// waves take interleaved quarters of the partial rows (8 loads in flight per lane), and the
-// quarters are added in a fixed order through LDS (deterministic).
+// Column sums over the G workgroup partials: a workgroup owns 64 of the NRED*D columns; its
+// 4 waves take interleaved quarters of the partial rows (8 loads in flight per lane), and
+// the quarters are added in a fixed order through LDS (deterministic).
 __global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float* __restrict__ partial, int G, int D,
-                                                                     float* __restrict__ dscale,
-                                                                     float* __restrict__ doffset) {
-  __shared__ float q[4][64];
+                                                                     int D1, float* __restrict__ dscale,
+                                                                     float* __restrict__ doffset,
+                                                                     float* __restrict__ dbB,
+                                                                     float* __restrict__ dbW) {
+  __shared__ float qs[4][64];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
   float s = 0.0f;
-  if (i < 2 * D) {
-    const int64_t stride = 2 * (int64_t)D;
+  if (i < NRED * D) {
+    const int64_t stride = (int64_t)NRED * D;
     int g = w;
     float a[8];
     for (; g + 28 < G; g += 32) {
@@ -220,22 +233,28 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float
     }
     for (; g < G; g += 4) s += partial[(int64_t)g * stride + i];
   }
-  q[w][lane] = s;
+  qs[w][lane] = s;
   __syncthreads();
-  if (w == 0 && i < 2 * D) {
-    const float t = (q[0][lane] + q[1][lane]) + (q[2][lane] + q[3][lane]);
-    if (i < D) {
-      dscale[i] = t;
-    } else {
-      doffset[i - D] = t;
+  if (w == 0 && i < NRED * D) {
+    const float t = (qs[0][lane] + qs[1][lane]) + (qs[2][lane] + qs[3][lane]);
+    const int q = i / D, c = i % D;
+    if (q == 0) {
+      dscale[c] = t;
+    } else if (q == 1) {
+      doffset[c] = t;
+    } else if (c < D1) {
+      if (dbB) dbB[c] = t;
+    } else if (dbW) {
+      dbW[c - D1] = t;
     }
   }
 }
 
-using FwdFn = void (*)(const float*, int64_t, int, const float*, int64_t, int, const float*, const float*, int, float,
-                       float, uint64_t, int, float*, int64_t, float*, float*);
-using BwdFn = void (*)(const float*, int64_t, const float*, int64_t, int, const float*, int64_t, int, const float*,
-                       const float*, const float*, int, float, float, uint64_t, int, float*, float*, float*);
+using FwdFn = void (*)(const float*, int64_t, const float*, int, const float*, int64_t, const float*, int,
+                       const float*, const float*, int, float, float, uint64_t, int, float*, int64_t, float*, float*);
+using BwdFn = void (*)(const float*, int64_t, const float*, int64_t, const float*, int, const float*, int64_t,
+                       const float*, int, const float*, const float*, const float*, int, float, float, uint64_t, int,
+                       float*, float*, float*);
 
 FwdFn fwd_fn(int nv) {
   switch (nv) {
@@ -266,7 +285,7 @@ BwdFn bwd_fn(int nv) {
 }
 
 int check_shapes(const char* fn, int64_t D1, int64_t D2, int64_t M, const void* hB, int64_t ldb, const void* hW,
-                 int64_t ldw) {
+                 int64_t ldw, const void* bB, const void* bW) {
   GNN_REQUIRE(M >= 0 && D1 >= 0 && D2 >= 0, "%s: negative size", fn);
   GNN_REQUIRE(M < INT_MAX, "%s: M too large", fn);
   GNN_REQUIRE(D1 % 4 == 0 && D2 % 4 == 0, "%s: D1 and D2 must be multiples of 4", fn);
@@ -274,6 +293,7 @@ int check_shapes(const char* fn, int64_t D1, int64_t D2, int64_t M, const void* 
               (long long)(D1 + D2));
   GNN_REQUIRE(D1 == 0 || (hB && ldb % 4 == 0 && (uintptr_t)hB % 16 == 0), "%s: hB must be 16-byte aligned rows", fn);
   GNN_REQUIRE(D2 == 0 || (hW && ldw % 4 == 0 && (uintptr_t)hW % 16 == 0), "%s: hW must be 16-byte aligned rows", fn);
+  GNN_REQUIRE((uintptr_t)bB % 16 == 0 && (uintptr_t)bW % 16 == 0, "%s: biases must be 16-byte aligned", fn);
   return 0;
 }
 
@@ -282,9 +302,10 @@ int check_shapes(const char* fn, int64_t D1, int64_t D2, int64_t M, const void* 
 extern "C" {
 
 int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float* hW, int64_t ldw, int64_t D2,
-                          const float* scale, const float* offset, int64_t M, float p_drop, uint64_t seed,
-                          int training, float* Y, int64_t ldy, float* mean_out, float* rstd_out, void* stream) {
-  int rc = check_shapes("gnn_sage_norm_fwd_f32", D1, D2, M, hB, ldb, hW, ldw);
+                          const float* biasB, const float* biasW, const float* scale, const float* offset, int64_t M,
+                          float p_drop, uint64_t seed, int training, float* Y, int64_t ldy, float* mean_out,
+                          float* rstd_out, void* stream) {
+  int rc = check_shapes("gnn_sage_norm_fwd_f32", D1, D2, M, hB, ldb, hW, ldw, biasB, biasW);
   if (rc) return rc;
   if (M == 0) return 0;
   GNN_REQUIRE(scale && offset && Y && mean_out && rstd_out, "gnn_sage_norm_fwd_f32: NULL pointer");
@@ -294,22 +315,24 @@ int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float*
   const int nv = (int)ceil_div(D, 256);
   hipStream_t st = (hipStream_t)stream;
   const float inv_keep = 1.0f / (1.0f - p_drop);
-  hipLaunchKernelGGL(fwd_fn(nv), dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, st, hB ? hB : hW, ldb, (int)D1, hW,
-                     ldw, D, scale, offset, (int)M, p_drop, inv_keep, seed, training, Y, ldy, mean_out, rstd_out);
+  hipLaunchKernelGGL(fwd_fn(nv), dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, st, hB ? hB : hW, ldb, biasB,
+                     (int)D1, hW, ldw, biasW, D, scale, offset, (int)M, p_drop, inv_keep, seed, training, Y, ldy,
+                     mean_out, rstd_out);
   GNN_LAUNCHED("sage_norm_fwd_kernel");
   return 0;
 }
 
 size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
   const int64_t G = M <= 0 ? 1 : (ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID);
-  return gnn::align_up((size_t)G * 2 * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
+  return gnn::align_up((size_t)G * NRED * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
 }
 
 int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
-                          int64_t ldw, int64_t D2, const float* scale, const float* mean, const float* rstd, int64_t M,
-                          float p_drop, uint64_t seed, int training, float* dhB, float* dhW, float* dscale,
-                          float* doffset, void* workspace, size_t workspace_bytes, void* stream) {
-  int rc = check_shapes("gnn_sage_norm_bwd_f32", D1, D2, M, hB, ldb, hW, ldw);
+                          int64_t ldw, int64_t D2, const float* biasB, const float* biasW, const float* scale,
+                          const float* mean, const float* rstd, int64_t M, float p_drop, uint64_t seed, int training,
+                          float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  int rc = check_shapes("gnn_sage_norm_bwd_f32", D1, D2, M, hB, ldb, hW, ldw, biasB, biasW);
   if (rc) return rc;
   GNN_REQUIRE(scale && dscale && doffset, "gnn_sage_norm_bwd_f32: NULL pointer");
   GNN_REQUIRE(p_drop >= 0.0f && p_drop < 1.0f, "gnn_sage_norm_bwd_f32: p_drop must be in [0, 1)");
@@ -318,6 +341,8 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
   if (M == 0) {
     GNN_HIP(hipMemsetAsync(dscale, 0, (size_t)D * 4, st), "dscale memset");
     GNN_HIP(hipMemsetAsync(doffset, 0, (size_t)D * 4, st), "doffset memset");
+    if (dbiasB && D1) GNN_HIP(hipMemsetAsync(dbiasB, 0, (size_t)D1 * 4, st), "dbiasB memset");
+    if (dbiasW && D2) GNN_HIP(hipMemsetAsync(dbiasW, 0, (size_t)D2 * 4, st), "dbiasW memset");
     return 0;
   }
   GNN_REQUIRE(gY && mean && rstd && (D1 == 0 || dhB) && (D2 == 0 || dhW), "gnn_sage_norm_bwd_f32: NULL pointer");
@@ -330,12 +355,12 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
   const int64_t G = ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID;
   const float inv_keep = 1.0f / (1.0f - p_drop);
   float* partial = (float*)workspace;
-  hipLaunchKernelGGL(bwd_fn(nv), dim3((unsigned)G), dim3(256), (size_t)8 * D * sizeof(float), st, gY, ldg,
-                     hB ? hB : hW, ldb, (int)D1, hW, ldw, D, scale, mean, rstd, (int)M, p_drop, inv_keep, seed,
-                     training, dhB ? dhB : dhW, dhW, partial);
+  hipLaunchKernelGGL(bwd_fn(nv), dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st, gY, ldg,
+                     hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop,
+                     inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
   GNN_LAUNCHED("sage_norm_bwd_kernel");
-  sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(2 * D, 64)), dim3(256), 0, st>>>(partial, (int)G, D, dscale,
-                                                                                          doffset);
+  sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(NRED * D, 64)), dim3(256), 0, st>>>(
+      partial, (int)G, D, (int)D1, dscale, doffset, dbiasB, dbiasW);
   GNN_LAUNCHED("sage_norm_bwd_finalize_kernel");
   return 0;
 }

@@ -130,7 +130,8 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
     int M, int nnz, int S, int nunits,
     const float* __restrict__ X, int64_t ldx,
     float* __restrict__ Y, int64_t ldy,
-    float* __restrict__ slab, int64_t ldslab, int F) {
+    float* __restrict__ slab, int64_t ldslab, int F,
+    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
   using V = typename Vec<VW>::T;
   constexpr int P = 64 / G;            // nonzeros taken side by side per step
   constexpr int COVER = VW * G * NJ;   // columns covered by one column tile
@@ -215,15 +216,24 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
     }
 
     float* dst;
+    const float* res = nullptr;  // residual row added to a complete output row
     if (rb >= ustart && re <= uend) {
       dst = Y + (int64_t)r * ldy;
+      if (rmap) {
+        const int q = rmap[r];
+        if (q >= 0) res = R + (int64_t)q * ldr;
+      }
     } else {
       dst = slab + ((int64_t)u * 2 + (rb < ustart ? 0 : 1)) * ldslab;
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int cc = c0 + j * G * VW;
-      if ((j % P) == sub && cc < F) *reinterpret_cast<V*>(dst + cc) = acc[j];
+      if ((j % P) == sub && cc < F) {
+        V a = acc[j];
+        if (res) a += *reinterpret_cast<const V*>(res + cc);
+        *reinterpret_cast<V*>(dst + cc) = a;
+      }
     }
   }
 }
@@ -235,7 +245,8 @@ template <int VW>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int* __restrict__ rowptr, int M, int S,
     const float* __restrict__ slab, int64_t ldslab,
-    float* __restrict__ Y, int64_t ldy, int F) {
+    float* __restrict__ Y, int64_t ldy, int F,
+    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
   using V = typename Vec<VW>::T;
   const int lane = threadIdx.x & 63;
   for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < M; r += gridDim.x * 4) {
@@ -245,6 +256,7 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int u0 = rb / S;
     const int u1 = (re - 1) / S;
     if (u0 == u1) continue;
+    const int q = rmap ? rmap[r] : -1;
     for (int cc = lane * VW; cc < F; cc += 64 * VW) {
       V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
       int u = u0 + 1;
@@ -259,6 +271,7 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
         s += a3;
       }
       for (; u <= u1; ++u) s += *reinterpret_cast<const V*>(slab + ((int64_t)u * 2) * ldslab + cc);
+      if (q >= 0) s += *reinterpret_cast<const V*>(R + (int64_t)q * ldr + cc);
       *reinterpret_cast<V*>(Y + (int64_t)r * ldy + cc) = s;
     }
   }
@@ -890,7 +903,7 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
 }
 
 using MainFn = void (*)(const int*, const int*, const float*, int, int, int, int, const float*, int64_t,
-                        float*, int64_t, float*, int64_t, int);
+                        float*, int64_t, float*, int64_t, int, const float*, int64_t, const int*);
 
 constexpr int pick_u(int nj) { return nj <= 4 ? 4 : (nj == 5 ? 3 : 2); }
 
@@ -1015,6 +1028,14 @@ void gnn_spmm_set_timing_events(void* start, void* stop) {
 int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val, int64_t M, int64_t K,
                      int64_t nnz, const float* X, int64_t ldx, float* Y, int64_t ldy, int64_t F,
                      void* workspace, size_t workspace_bytes, int64_t unit_nnz, void* stream) {
+  return gnn_spmm_csr_f32_ex(rowptr, col, val, M, K, nnz, X, ldx, Y, ldy, F, nullptr, 0, nullptr, workspace,
+                             workspace_bytes, unit_nnz, stream);
+}
+
+int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* val, int64_t M, int64_t K,
+                        int64_t nnz, const float* X, int64_t ldx, float* Y, int64_t ldy, int64_t F,
+                        const float* R, int64_t ldr, const int32_t* rmap, void* workspace, size_t workspace_bytes,
+                        int64_t unit_nnz, void* stream) {
   hipEvent_t ev0 = g_ev_start, ev1 = g_ev_stop;
   g_ev_start = g_ev_stop = nullptr;
   GNN_REQUIRE(M >= 0 && K >= 0 && nnz >= 0 && F >= 0, "gnn_spmm_csr_f32: negative size");
@@ -1024,6 +1045,7 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
   if (M == 0 || F == 0) return 0;
   GNN_REQUIRE(rowptr && Y, "gnn_spmm_csr_f32: NULL rowptr/Y");
   GNN_REQUIRE(nnz == 0 || (col && val && X), "gnn_spmm_csr_f32: NULL col/val/X");
+  GNN_REQUIRE(rmap == nullptr || (R != nullptr && F <= ldr), "gnn_spmm_csr_f32_ex: rmap needs R with F <= ldr");
   const SpmmCfg c = make_cfg(M, K, nnz, F, ldx, ldy, X, Y, unit_nnz);
   GNN_REQUIRE(c.nunits * c.unit < (int64_t)INT_MAX + c.unit, "gnn_spmm_csr_f32: unit overflow");
   GNN_REQUIRE(c.nunits <= (int64_t)INT_MAX / 2, "gnn_spmm_csr_f32: too many units");
@@ -1032,6 +1054,8 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
   GNN_REQUIRE(!any_split || (workspace && workspace_bytes >= need),
               "gnn_spmm_csr_f32: workspace too small (%zu < %zu)", workspace_bytes, need);
   GNN_REQUIRE((uintptr_t)workspace % 16 == 0, "gnn_spmm_csr_f32: workspace not 16-byte aligned");
+  GNN_REQUIRE(rmap == nullptr || (ldr % c.vw == 0 && (uintptr_t)R % (4 * c.vw) == 0),
+              "gnn_spmm_csr_f32_ex: R (ldr %lld) not aligned for %d-wide vectors", (long long)ldr, c.vw);
   MainFn fn = select_main(c);
   GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no kernel for vw=%d g=%d nj=%d", c.vw, c.g, c.nj);
   hipStream_t st = (hipStream_t)stream;
@@ -1039,20 +1063,23 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
   const dim3 grid((unsigned)ceil_div(c.nunits, 4), (unsigned)c.tiles);
   if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
   hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
-                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F);
+                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap);
   GNN_LAUNCHED("spmm_unit_kernel");
   if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
     const dim3 g2((unsigned)std::min<int64_t>(ceil_div(M, 4), 512));
     switch (c.vw) {
       case 4:
-        spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
+                                                         R, ldr, (const int*)rmap);
         break;
       case 2:
-        spmm_combine_kernel<2><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        spmm_combine_kernel<2><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
+                                                         R, ldr, (const int*)rmap);
         break;
       default:
-        spmm_combine_kernel<1><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F);
+        spmm_combine_kernel<1><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
+                                                         R, ldr, (const int*)rmap);
         break;
     }
     GNN_LAUNCHED("spmm_combine_kernel");

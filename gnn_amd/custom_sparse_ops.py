@@ -163,9 +163,13 @@ def csr_of(mat: "torch.Tensor | CsrOperand") -> CsrOperand:
     return plan
 
 
-def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: int = 0) -> torch.Tensor:
+def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: int = 0,
+             residual: Optional[torch.Tensor] = None, rmap: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Y = A·X on the GPU. ``dense`` must be fp32, row-major rows (stride(1) == 1); a padded
-    row stride (stride(0) > F) is accepted and read in place."""
+    row stride (stride(0) > F) is accepted and read in place.
+
+    With ``rmap`` (int32[M], -1 = none) the rows ``residual[rmap[r]]`` are added to the
+    output rows in the same kernel (gnn_spmm_csr_f32_ex)."""
     _require(dense.is_cuda, "denseMat must be a CUDA tensor")
     _require(dense.dim() == 2, "denseMat must be 2-D")
     _require(dense.dtype == torch.float32, "denseMat must be float32")
@@ -179,8 +183,15 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
     # Padded rows (the layer-0 staging buffer: 602 floats in 604-float rows): let the
     # kernel run over the padded width Fk = round_up(F, 4) so it can use 16-byte loads, into
     # an output with the same padded stride; the caller gets the (M x F) view.
+    if rmap is not None:
+        _require(residual is not None and residual.is_cuda and residual.dtype == torch.float32,
+                 "residual must be a float32 CUDA tensor")
+        _require(rmap.is_cuda and rmap.dtype == torch.int32 and rmap.is_contiguous() and rmap.numel() == M,
+                 "rmap must be a contiguous int32 CUDA tensor of M entries")
+        _require(residual.dim() == 2 and residual.shape[1] == F and residual.stride(1) == 1,
+                 "residual rows must be contiguous with F columns")
     Fk = F
-    if F % 4 and ldx % 4 == 0 and dense.data_ptr() % 16 == 0:
+    if F % 4 and ldx % 4 == 0 and dense.data_ptr() % 16 == 0 and rmap is None:
         F4 = F + (4 - F % 4)
         avail = dense.untyped_storage().nbytes() // 4 - dense.storage_offset()
         if ldx >= F4 and (K - 1) * ldx + F4 <= avail:
@@ -200,9 +211,16 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
             e1.record()
             L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
             _timing_records.append((tag, e0, e1, algorithmic_bytes(M, op.nnz, F)))
-        _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
-                                      dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
-                                      ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32")
+        if rmap is None:
+            _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
+                                          dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
+                                          ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32")
+        else:
+            ldr = residual.stride(0) if residual.shape[0] > 1 else max(F, 1)
+            _lib.check(L.gnn_spmm_csr_f32_ex(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
+                                             dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
+                                             residual.data_ptr(), ldr, rmap.data_ptr(),
+                                             ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32_ex")
     return out if Fk == F else out[:, :F]
 
 

@@ -1,7 +1,7 @@
 """Fused layer epilogue of GraphSAGE / GCN (HIP, include/gnn_layers.h) as an autograd op.
 
-``sage_norm(hB, hW, scale, offset, p, training)`` computes, per row,
-    dropout_p( (elu(cat[hB, hW]) - mean) * scale * rsqrt(var + 1e-9) + offset )
+``sage_norm(hB, hW, scale, offset, p, training, biasB, biasW)`` computes, per row,
+    dropout_p( (elu(cat[hB + biasB, hW + biasW]) - mean) * scale * rsqrt(var + 1e-9) + offset )
 which is GraphSageConvolution.forward's tail (models.py:18-25) plus the dropout that
 GraphSage.forward applies to every layer output (models.py:43); with hB = None it is
 GraphConvolution's (models.py:58-64, 82). One HIP pass forward, one (+ a column reduction)
@@ -28,14 +28,18 @@ def _stream(dev) -> int:
 
 class SageNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, hB, hW, scale, offset, p: float, training: bool, seed: int):
-        for t in (hW, scale, offset) + ((hB,) if hB is not None else ()):
+    def forward(ctx, hB, hW, scale, offset, biasB, biasW, p: float, training: bool, seed: int):
+        for t in (hW, scale, offset) + tuple(t for t in (hB, biasB, biasW) if t is not None):
             if not t.is_cuda:
                 raise RuntimeError("sage_norm: tensors must be CUDA tensors")
             if t.dtype != torch.float32:
                 raise RuntimeError("sage_norm: tensors must be float32")
         hW = hW.contiguous()
         hB = hB.contiguous() if hB is not None else None
+        if hB is None:
+            biasB = None
+        biasB = biasB.contiguous() if biasB is not None else None
+        biasW = biasW.contiguous() if biasW is not None else None
         M, D2 = hW.shape
         D1 = 0 if hB is None else hB.shape[1]
         D = D1 + D2
@@ -46,19 +50,16 @@ class SageNormFn(torch.autograd.Function):
         mean = torch.empty(M, dtype=torch.float32, device=dev)
         rstd = torch.empty(M, dtype=torch.float32, device=dev)
         L = _lib.lib()
-        _lib.check(L.gnn_sage_norm_fwd_f32(_ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(scale), _ptr(offset), M,
-                                           float(p), seed, int(training), _ptr(Y), D, _ptr(mean), _ptr(rstd),
-                                           _stream(dev)), "gnn_sage_norm_fwd_f32")
-        ctx.save_for_backward(hB if hB is not None else hW, hW, scale, mean, rstd)
-        ctx.has_b = hB is not None
+        _lib.check(L.gnn_sage_norm_fwd_f32(_ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(biasB), _ptr(biasW),
+                                           _ptr(scale), _ptr(offset), M, float(p), seed, int(training), _ptr(Y), D,
+                                           _ptr(mean), _ptr(rstd), _stream(dev)), "gnn_sage_norm_fwd_f32")
+        ctx.save_for_backward(hB, hW, scale, mean, rstd, biasB, biasW)
         ctx.cfg = (float(p), int(training), int(seed))
         return Y
 
     @staticmethod
     def backward(ctx, gY):
-        hB, hW, scale, mean, rstd = ctx.saved_tensors
-        if not ctx.has_b:
-            hB = None
+        hB, hW, scale, mean, rstd, biasB, biasW = ctx.saved_tensors
         p, training, seed = ctx.cfg
         gY = gY.contiguous()
         M, D2 = hW.shape
@@ -68,14 +69,59 @@ class SageNormFn(torch.autograd.Function):
         dhW = torch.empty_like(hW)
         dscale = torch.empty(D1 + D2, dtype=torch.float32, device=dev)
         doffset = torch.empty(D1 + D2, dtype=torch.float32, device=dev)
+        dbB = torch.empty_like(biasB) if biasB is not None else None
+        dbW = torch.empty_like(biasW) if biasW is not None else None
         L = _lib.lib()
         wsb = L.gnn_sage_norm_bwd_workspace_bytes(M, D1 + D2)
         ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
-        _lib.check(L.gnn_sage_norm_bwd_f32(_ptr(gY), D1 + D2, _ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(scale),
-                                           _ptr(mean), _ptr(rstd), M, p, seed, training, _ptr(dhB), _ptr(dhW),
-                                           _ptr(dscale), _ptr(doffset), _ptr(ws), wsb, _stream(dev)),
+        _lib.check(L.gnn_sage_norm_bwd_f32(_ptr(gY), D1 + D2, _ptr(hB), D1 or 4, D1, _ptr(hW), D2, D2, _ptr(biasB),
+                                           _ptr(biasW), _ptr(scale), _ptr(mean), _ptr(rstd), M, p, seed, training,
+                                           _ptr(dhB), _ptr(dhW), _ptr(dscale), _ptr(doffset), _ptr(dbB), _ptr(dbW),
+                                           _ptr(ws), wsb, _stream(dev)),
                    "gnn_sage_norm_bwd_f32")
-        return dhB, dhW, dscale, doffset, None, None, None
+        return dhB, dhW, dscale, doffset, dbB, dbW, None, None, None
+
+
+class SageAggregateFn(torch.autograd.Function):
+    """Both inputs of GraphSageConvolution (models.py:18-21): (A·x, x[sampled]).
+
+    Forward: the HIP aggregation and the HIP row gather. Backward: ONE aggregation kernel
+    d(x) = Aᵀ·d(A·x) + scatter(d(x[sampled])) — the scatter is fused into its row stores as a
+    residual (gnn_spmm_csr_f32_ex with rmap[sampled[i]] = i), instead of zeros + scatter +
+    an autograd add over the whole K x F gradient. ``sampled`` rows must be unique (they are
+    positions of the previous layer's nodes, sampler.py:143)."""
+
+    @staticmethod
+    def forward(ctx, adj, x, sampled):
+        from . import custom_sparse_ops as cso
+
+        op = cso.csr_of(adj)
+        feat = cso.spmm_csr(op, x, tag="fwd")
+        xs = torch.empty((sampled.numel(), x.shape[1]), dtype=x.dtype, device=x.device)
+        cso.gather_rows(x, sampled, xs, None, n=sampled.numel())
+        ctx.op = op
+        ctx.save_for_backward(sampled)
+        return feat, xs
+
+    @staticmethod
+    def backward(ctx, g_feat, g_xs):
+        from . import custom_sparse_ops as cso
+
+        if not ctx.needs_input_grad[1]:
+            return None, None, None
+        (sampled,) = ctx.saved_tensors
+        op_t = ctx.op.transpose()
+        K = op_t.shape[0]
+        rmap = torch.full((K,), -1, dtype=torch.int32, device=sampled.device)
+        rmap[sampled] = torch.arange(sampled.numel(), dtype=torch.int32, device=sampled.device)
+        return None, cso.spmm_csr(op_t, g_feat.contiguous(), tag="bwd", residual=g_xs.contiguous(), rmap=rmap), None
+
+
+def sage_aggregate(adj, x: torch.Tensor, sampled: torch.Tensor):
+    """(A·x, x[sampled]) with the fused backward of SageAggregateFn."""
+    if sampled.dtype != torch.int64 or not sampled.is_contiguous():
+        sampled = sampled.long().contiguous()
+    return SageAggregateFn.apply(adj, x, sampled)
 
 
 class IndexRowsFn(torch.autograd.Function):
@@ -111,6 +157,9 @@ def index_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 
 def sage_norm(hB: Optional[torch.Tensor], hW: torch.Tensor, scale: torch.Tensor, offset: torch.Tensor,
-              p: float = 0.0, training: bool = False) -> torch.Tensor:
+              p: float = 0.0, training: bool = False, biasB: Optional[torch.Tensor] = None,
+              biasW: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """hB / hW are the bias-free linear outputs; the linear biases (optional) are added, and
+    their gradients reduced, inside the fused kernels."""
     seed = int(torch.randint(0, 2**62, (1,)).item()) if (training and p > 0) else 0
-    return SageNormFn.apply(hB, hW, scale, offset, float(p), bool(training and p > 0), seed)
+    return SageNormFn.apply(hB, hW, scale, offset, biasB, biasW, float(p), bool(training and p > 0), seed)

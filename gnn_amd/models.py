@@ -49,13 +49,17 @@ class GraphSageConvolution(nn.Module):
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
     def forward_fused(self, x, adj, sampled_nodes, p, training):
-        from .fused import index_rows, sage_norm
+        from .fused import index_rows, sage_aggregate, sage_norm
 
+        bB, bW = self.linearB.bias, self.linearW.bias
         if self.order > 0:
-            feat = self.spmm_fn(adj, x)
-            xs = index_rows(x, sampled_nodes)
-            return sage_norm(self.linearB(xs), self.linearW(feat), self.scale, self.offset, p, training)
-        return sage_norm(None, self.linearW(x), self.scale, self.offset, p, training)
+            if self.spmm_fn is _default_spmm:
+                feat, xs = sage_aggregate(adj, x, sampled_nodes)
+            else:
+                feat, xs = self.spmm_fn(adj, x), index_rows(x, sampled_nodes)
+            return sage_norm(F.linear(xs, self.linearB.weight), F.linear(feat, self.linearW.weight), self.scale,
+                             self.offset, p, training, bB, bW)
+        return sage_norm(None, F.linear(x, self.linearW.weight), self.scale, self.offset, p, training, None, bW)
 
 
 class GraphSage(nn.Module):
@@ -107,7 +111,8 @@ class GraphConvolution(nn.Module):
         from .fused import sage_norm
 
         feat = self.spmm_fn(adj, x) if self.order > 0 else x
-        return sage_norm(None, self.linear(feat), self.scale, self.offset, p, training)
+        return sage_norm(None, F.linear(feat, self.linear.weight), self.scale, self.offset, p, training, None,
+                         self.linear.bias)
 
 
 class GCN(nn.Module):

@@ -4,12 +4,14 @@
  * Replaces the elementwise tail of GraphSageConvolution.forward (models.py:18-25) and
  * GraphConvolution.forward (models.py:58-64), plus the dropout GraphSage/GCN apply to each
  * layer's output (models.py:43,82):
- *     h   = cat([hB, hW], 1)                      (GCN: h = hW, D1 = 0)
+ *     h   = cat([hB + biasB, hW + biasW], 1)      (GCN: h = hW + biasW, D1 = 0)
  *     o   = elu(h)
  *     y   = (o - mean(o)) * scale * rsqrt(var(o) + 1e-9) + offset     (biased var, per row)
  *     out = dropout(y, p)                          (training only; inverted scaling)
  * in ONE pass over the rows (one wave per row, the row held in registers), and its
- * backward in one more pass plus a deterministic column reduction for d(scale), d(offset).
+ * backward in one more pass plus a deterministic column reduction for d(scale), d(offset)
+ * and the linear biases' gradients d(biasB), d(biasW) (hB / hW are the bias-free linear
+ * outputs; biases may be NULL, then their gradients are not written).
  * Dropout masks come from a counter-based hash of (seed, row * D + col): nothing is stored,
  * backward regenerates them.
  *
@@ -27,15 +29,17 @@ extern "C" {
 #endif
 
 int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float* hW, int64_t ldw, int64_t D2,
-                          const float* scale, const float* offset, int64_t M, float p_drop, uint64_t seed,
-                          int training, float* Y, int64_t ldy, float* mean_out, float* rstd_out, void* stream);
+                          const float* biasB, const float* biasW, const float* scale, const float* offset, int64_t M,
+                          float p_drop, uint64_t seed, int training, float* Y, int64_t ldy, float* mean_out,
+                          float* rstd_out, void* stream);
 
 size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D);
 
 int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
-                          int64_t ldw, int64_t D2, const float* scale, const float* mean, const float* rstd, int64_t M,
-                          float p_drop, uint64_t seed, int training, float* dhB, float* dhW, float* dscale,
-                          float* doffset, void* workspace, size_t workspace_bytes, void* stream);
+                          int64_t ldw, int64_t D2, const float* biasB, const float* biasW, const float* scale,
+                          const float* mean, const float* rstd, int64_t M, float p_drop, uint64_t seed, int training,
+                          float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

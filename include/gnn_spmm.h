@@ -58,6 +58,20 @@ int gnn_spmm_csr_f32(const int32_t* rowptr, const int32_t* col, const float* val
                      void* workspace, size_t workspace_bytes, int64_t unit_nnz,
                      void* stream);
 
+/* Same, plus a row-mapped residual fused into the stores:
+ *     Y[r, :] = (A · X)[r, :] + (rmap[r] >= 0 ? R[rmap[r], :] : 0)
+ * rmap (int32, M entries, device) may be NULL (then R is ignored). This is the backward of
+ * GraphSageConvolution's two inputs (models.py:18-21): d(x) = A^T · d(A·x) + scatter of
+ * d(x[sampled]) — the scatter is the residual with rmap = inverse of the sampled-row map.
+ * R rows are read with stride ldr (F <= ldr) and must be aligned like Y. */
+int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* val,
+                        int64_t M, int64_t K, int64_t nnz,
+                        const float* X, int64_t ldx,
+                        float* Y, int64_t ldy, int64_t F,
+                        const float* R, int64_t ldr, const int32_t* rmap,
+                        void* workspace, size_t workspace_bytes, int64_t unit_nnz,
+                        void* stream);
+
 /* Describe the kernel configuration gnn_spmm_csr_f32 would pick (vector width, lanes per
  * column group, column chunks per lane, column tiles, units). For diagnostics/benchmarks. */
 int gnn_spmm_config(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,

@@ -17,7 +17,11 @@ from gnn_amd.models import build_model, loss
 pytestmark = pytest.mark.gpu
 
 
-def _ref(hB, hW, scale, offset):
+def _ref(hB, hW, scale, offset, bB=None, bW=None):
+    if bW is not None:
+        hW = hW + bW
+    if hB is not None and bB is not None:
+        hB = hB + bB
     h = hW if hB is None else torch.cat([hB, hW], 1)
     out = F.elu(h)
     mean = out.mean(dim=1).view(out.shape[0], 1)
@@ -25,22 +29,25 @@ def _ref(hB, hW, scale, offset):
     return (out - mean) * scale * torch.rsqrt(var) + offset
 
 
+@pytest.mark.parametrize("bias", [False, True])
 @pytest.mark.parametrize("D1,D2,M", [(512, 512, 1000), (0, 512, 777), (512, 512, 1), (256, 256, 5), (0, 100, 33),
                                      (1024, 1024, 300)])
-def test_sage_norm_matches_torch(dev, D1, D2, M):
+def test_sage_norm_matches_torch(dev, D1, D2, M, bias):
     g = torch.Generator().manual_seed(D1 + D2 + M)
     hB = torch.randn(M, D1, generator=g) * 2 if D1 else None
     hW = torch.randn(M, D2, generator=g) * 2
     scale = torch.rand(D1 + D2, generator=g) + 0.5
     offset = torch.randn(D1 + D2, generator=g)
+    bB = torch.randn(D1, generator=g) if (bias and D1) else None
+    bW = torch.randn(D2, generator=g) if bias else None
     gY = torch.randn(M, D1 + D2, generator=g)
     # fp64 reference on the CPU
-    leaves64 = [t.double().requires_grad_(True) if t is not None else None for t in (hB, hW, scale, offset)]
+    leaves64 = [t.double().requires_grad_(True) if t is not None else None for t in (hB, hW, scale, offset, bB, bW)]
     y64 = _ref(*leaves64)
     y64.backward(gY.double())
     # fused on the GPU
-    leaves = [t.to(dev).requires_grad_(True) if t is not None else None for t in (hB, hW, scale, offset)]
-    y = sage_norm(*leaves, p=0.1, training=False)
+    leaves = [t.to(dev).requires_grad_(True) if t is not None else None for t in (hB, hW, scale, offset, bB, bW)]
+    y = sage_norm(*leaves[:4], p=0.1, training=False, biasB=leaves[4], biasW=leaves[5])
     y.backward(gY.to(dev))
     np.testing.assert_allclose(y.detach().cpu().numpy(), y64.detach().numpy(), rtol=1e-4, atol=1e-5)
     for a, b in zip(leaves, leaves64):

@@ -68,6 +68,54 @@ def test_forward_unit_splits(dev, unit):
     _check_fwd(dev, M, K, 64, lens, seed=unit + 1, unit_nnz=unit)
 
 
+@pytest.mark.parametrize("unit,F", [(0, 64), (1, 64), (7, 602), (64, 100), (0, 512), (333, 3)])
+def test_residual_rows(dev, unit, F):
+    """gnn_spmm_csr_f32_ex: Y = A·X + R[rmap[r]] for rows with rmap >= 0, in complete rows and
+    in rows combined across units (split rows), empty rows included."""
+    M, K = 180, 300
+    rng = np.random.default_rng(unit * 31 + F)
+    lens = powerlaw_lens(M, 40, 1.3, rng, K)
+    lens[::13] = 0
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    R = rng.standard_normal((M // 2, F)).astype(np.float32)
+    rmap = np.full(M, -1, np.int32)
+    pick = rng.choice(M, M // 2, replace=False)
+    rmap[pick] = np.arange(M // 2, dtype=np.int32)
+    Yref = O.spmm_f32(rowptr, ocol, oval, X)
+    Yref[pick] += R
+    Y = cso.spmm_csr(op, torch.from_numpy(X).to(dev), unit_nnz=unit, residual=torch.from_numpy(R).to(dev),
+                     rmap=torch.from_numpy(rmap).to(dev))
+    np.testing.assert_allclose(Y.cpu().numpy(), Yref, rtol=RTOL, atol=ATOL)
+
+
+def test_sage_aggregate_backward(dev):
+    """The fused GraphSAGE aggregation backward equals spmm backward + index_rows backward
+    (the autograd sum of the two), bit for bit."""
+    from gnn_amd.fused import index_rows, sage_aggregate
+
+    M, K, F = 400, 900, 96
+    rng = np.random.default_rng(11)
+    lens = powerlaw_lens(M, 60, 1.3, rng, K)
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    adj = cso.create_coo_tensor(t(full), t(rowptr), t(col), t(nf), M, K)
+    sampled = t(np.sort(rng.choice(K, M, replace=False)).astype(np.int64))
+    x = torch.randn(K, F, device=dev)
+    g1 = torch.randn(M, F, device=dev)
+    g2 = torch.randn(M, F, device=dev)
+    xa = x.clone().requires_grad_(True)
+    fa, sa = sage_aggregate(adj, xa, sampled)
+    (fa * g1 + sa * g2).sum().backward()
+    xb = x.clone().requires_grad_(True)
+    fb, sb = cso.spmm(adj, xb), index_rows(xb, sampled)
+    (fb * g1 + sb * g2).sum().backward()
+    assert torch.equal(fa, fb) and torch.equal(sa, sb)
+    assert torch.equal(xa.grad, xb.grad)
+
+
 def test_forward_padded_stride(dev):
     """X with a padded row stride (the staging buffer's 608-float rows) read in place."""
     M, K = 300, 500
