@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic child run")
     ap.add_argument("--unfused", action="store_true", help="torch elementwise layer tail instead of the HIP one")
+    ap.add_argument("--torch-profile", default="", help="after the timed run, write a torch.profiler op table here")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     return ap.parse_args()
 
@@ -238,6 +239,23 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     recs = cso.take_timing_records()
+    if args.torch_profile and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+            run(3, 0)
+            torch.cuda.synchronize()
+        with open(args.torch_profile, "w") as fh:
+            fh.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
+                                                                        max_name_column_width=60,
+                                                                        max_shapes_column_width=90))
+            fh.write("\n\n")
+            for ev in prof.events():
+                if ev.device_type.name == "CUDA":
+                    continue
+                if ev.name in ("aten::mm", "aten::addmm", "aten::linear", "aten::matmul"):
+                    kern = [(k.name[:70], round(float(getattr(k, "duration", 0)), 1)) for k in ev.kernels]
+                    fh.write(f"{ev.name} {ev.input_shapes} {kern}\n")
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
     # ---------------------------------------------------------------- roofline

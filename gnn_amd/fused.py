@@ -124,6 +124,51 @@ def sage_aggregate(adj, x: torch.Tensor, sampled: torch.Tensor):
     return SageAggregateFn.apply(adj, x, sampled)
 
 
+class _BlasLibrary:
+    """Route the GEMMs issued inside the block to one BLAS backend ("cublas" = rocBLAS,
+    "cublaslt" = hipBLASLt on ROCm builds of torch); restores the previous choice."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.prev = torch.backends.cuda.preferred_blas_library()
+        torch.backends.cuda.preferred_blas_library(self.name)
+
+    def __exit__(self, *exc):
+        torch.backends.cuda.preferred_blas_library(self.prev)
+        return False
+
+
+class LinearNoBiasFn(torch.autograd.Function):
+    """y = x·Wᵀ (the bias lives in the fused epilogue). Same math as F.linear; the backward
+    picks the BLAS backend per GEMM from measurements on MI355X (scripts/gemm_layouts.py):
+    the weight gradient Gᵀ·X (a long reduction over the sampled rows) runs 1.7-1.9x faster
+    on hipBLASLt than on rocBLAS at these shapes, while rocBLAS wins the forward / input
+    gradient."""
+
+    @staticmethod
+    def forward(ctx, x, W):
+        ctx.save_for_backward(x, W)
+        return torch.mm(x, W.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, W = ctx.saved_tensors
+        dx = torch.mm(g, W) if ctx.needs_input_grad[0] else None
+        dW = None
+        if ctx.needs_input_grad[1]:
+            with _BlasLibrary("cublaslt"):
+                dW = torch.mm(g.t(), x)
+        return dx, dW
+
+
+def linear_nobias(x: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    if x.is_cuda:
+        return LinearNoBiasFn.apply(x, W)
+    return torch.nn.functional.linear(x, W)
+
+
 class IndexRowsFn(torch.autograd.Function):
     """x[idx] for UNIQUE row indices (sampled_nodes: positions of the previous layer's nodes
     among the sampled ones, sampler.py:143). Forward: HIP row gather (reads strided rows in

@@ -49,7 +49,7 @@ class GraphSageConvolution(nn.Module):
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
     def forward_fused(self, x, adj, sampled_nodes, p, training):
-        from .fused import index_rows, sage_aggregate, sage_norm
+        from .fused import index_rows, linear_nobias, sage_aggregate, sage_norm
 
         bB, bW = self.linearB.bias, self.linearW.bias
         if self.order > 0:
@@ -57,9 +57,10 @@ class GraphSageConvolution(nn.Module):
                 feat, xs = sage_aggregate(adj, x, sampled_nodes)
             else:
                 feat, xs = self.spmm_fn(adj, x), index_rows(x, sampled_nodes)
-            return sage_norm(F.linear(xs, self.linearB.weight), F.linear(feat, self.linearW.weight), self.scale,
-                             self.offset, p, training, bB, bW)
-        return sage_norm(None, F.linear(x, self.linearW.weight), self.scale, self.offset, p, training, None, bW)
+            hB = linear_nobias(xs, self.linearB.weight)
+            hW = linear_nobias(feat, self.linearW.weight)
+            return sage_norm(hB, hW, self.scale, self.offset, p, training, bB, bW)
+        return sage_norm(None, linear_nobias(x, self.linearW.weight), self.scale, self.offset, p, training, None, bW)
 
 
 class GraphSage(nn.Module):
@@ -108,10 +109,10 @@ class GraphConvolution(nn.Module):
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
     def forward_fused(self, x, adj, p, training):
-        from .fused import sage_norm
+        from .fused import linear_nobias, sage_norm
 
         feat = self.spmm_fn(adj, x) if self.order > 0 else x
-        return sage_norm(None, F.linear(feat, self.linear.weight), self.scale, self.offset, p, training, None,
+        return sage_norm(None, linear_nobias(feat, self.linear.weight), self.scale, self.offset, p, training, None,
                          self.linear.bias)
 
 
