@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic child run")
     ap.add_argument("--unfused", action="store_true", help="torch elementwise layer tail instead of the HIP one")
+    ap.add_argument("--e2e-steps", type=int, default=60, help="steps of the live-sampling end-to-end run")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the live-sampling end-to-end run")
+    ap.add_argument("--workers", type=int, default=0, help="sampler threads per rank (0: auto)")
     ap.add_argument("--torch-profile", default="", help="after the timed run, write a torch.profiler op table here")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     return ap.parse_args()
@@ -160,6 +163,63 @@ def cpu_baseline(args, hb, feats, num_classes):
                       f"pre-sampled batch 0 (samp {args.samp_num}, bs {args.batch_size}), {dt:.1f} s"}
 
 
+def default_workers(world: int) -> int:
+    # the GPU box grants ~16 host CPUs per GPU (os.cpu_count() shows the whole machine)
+    return max(2, min(10, (os.cpu_count() or 8) // max(world, 1) - 4))
+
+
+def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):
+    """Mini-batches/s with sampling in the loop: the native LADIES sampler + host-row staging
+    in worker threads (gnn_amd.loader.BatchLoader) feeding the same training step. Also the
+    single-thread sampler cost per batch, native and numpy (rank 0)."""
+    from gnn_amd.loader import BatchLoader
+
+    workers = args.workers or default_workers(world)
+    ld = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pl.device_id_of_nodes_group[rank],
+                     pl.idx_of_nodes_on_device_group[rank], rank=rank, world_size=world, store=store,
+                     workers=workers, seed=4242)
+    it = ld.forever()
+
+    def nxt():
+        lb = next(it)
+        return lb.plan, lb.host.to_device(dev, build=False)
+
+    warm = max(2 * workers, 10)
+    pipeline(nxt, warm)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    pipeline(nxt, args.e2e_steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    ld.close()
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    out = {"value": round(world * args.e2e_steps / el, 3), "unit": "mini-batches/s", "steps": args.e2e_steps,
+           "sampler_workers_per_rank": workers,
+           "what": "live LADIES sampling (native, worker threads) + pinned host staging + H2D + the same step"}
+    if rank == 0:
+        chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
+        sm = np.array([args.samp_num] * 5)
+        pdev, pidx = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
+        t = time.perf_counter()
+        for i, c in enumerate(chunks[:3]):
+            sampler.ladies_sample_host(i, c, sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0,
+                                       list(range(world)))
+        nat = (time.perf_counter() - t) / 3
+        t = time.perf_counter()
+        sampler.ladies_sample_host(3, chunks[3], sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0,
+                                   list(range(world)), native=False)
+        npy = time.perf_counter() - t
+        out["sampler_ms_per_batch_1thread"] = {"native": round(nat * 1e3, 1), "numpy": round(npy * 1e3, 1)}
+    return out
+
+
 def main():
     args = parse()
     rank, world, local = init_distributed()
@@ -209,18 +269,31 @@ def main():
 
     nb = len(dbatches)
 
-    def run(steps, start, timing=False):
-        staged = stager.issue(plans[start % nb])
+    def pipeline(next_item, steps):
+        """next_item() -> (StagePlan, DeviceBatch). X0 staging of batch i+1 is issued on the
+        side stream before batch i's step, so its copies overlap that step's kernels."""
         loss = None
+        cur = next_item()
+        staged = stager.issue(cur[0])
         for i in range(steps):
-            j = (start + i) % nb
-            nxt = stager.issue(plans[(j + 1) % nb]) if i + 1 < steps else None
+            nxt = next_item() if i + 1 < steps else None
+            staged_next = stager.issue(nxt[0]) if nxt is not None else None
             x0 = staged.wait()
-            db = dbatches[j]
+            db = cur[1]
             adjs = db.build_operands()
             loss = trainer.step(x0, adjs, db.sampled_nodes, db.labels)
-            staged = nxt
+            cur, staged = nxt, staged_next
         return loss
+
+    def run(steps, start):
+        """Pre-sampled batches, operands resident in HBM, cycled (the headline step)."""
+        k = [start]
+
+        def nxt():
+            j = k[0] % nb
+            k[0] += 1
+            return plans[j], dbatches[j]
+        return pipeline(nxt, steps)
 
     run(args.warmup, 0)
     cso.enable_timing(not args.no_roofline)
@@ -239,6 +312,11 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     recs = cso.take_timing_records()
+
+    # ------------------------------------------------- end to end, live sampling
+    e2e = None
+    if not args.no_e2e and args.e2e_steps > 0:
+        e2e = end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev)
     if args.torch_profile and rank == 0:
         from torch.profiler import ProfilerActivity, profile
 
@@ -320,6 +398,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "spmm_per_callsite": spmm_detail,
+            "end_to_end": e2e,
             "final_loss": round(final_loss, 5),
         }
         print(json.dumps(line), flush=True)

@@ -50,6 +50,23 @@ _SIGNATURES = {
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
 
+# libgnn_sampler.so (include/gnn_sampler.h): host-only, g++
+SAMPLER_PATH = os.path.join(_HERE, "libgnn_sampler.so")
+_SAMPLER_SIGNATURES = {
+    "gnn_sampler_last_error": (ctypes.c_char_p, []),
+    "gnn_ladies_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
+                                 ctypes.POINTER(_VP)]),
+    "gnn_ladies_layer_dims": (_INT, [_VP, ctypes.c_int32, ctypes.POINTER(_I64)]),
+    "gnn_ladies_layer_copy": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP]),
+    "gnn_ladies_num_input_nodes": (_I64, [_VP]),
+    "gnn_ladies_input_nodes": (_INT, [_VP, _VP]),
+    "gnn_ladies_free": (None, [_VP]),
+    "gnn_mt19937_random_sample": (_INT, [ctypes.c_uint32, _I64, _VP]),
+    "gnn_host_gather_rows_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _I64]),
+}
+SAMPLER_EXPORTED_SYMBOLS = tuple(_SAMPLER_SIGNATURES)
+_sampler = None
+
 
 def lib() -> ctypes.CDLL:
     """Load (once) and return the HIP library. Raises if it is missing: no fallback."""
@@ -69,6 +86,31 @@ def lib() -> ctypes.CDLL:
                 fn.argtypes = args
             _lib = handle
     return _lib
+
+
+def sampler_lib() -> ctypes.CDLL:
+    """Load (once) the host sampler library. Raises if it is missing."""
+    global _sampler
+    if _sampler is not None:
+        return _sampler
+    with _lock:
+        if _sampler is None:
+            if not os.path.exists(SAMPLER_PATH):
+                raise RuntimeError(f"gnn_amd: native sampler {SAMPLER_PATH} is missing; build it with "
+                                   "`python -c 'import __graft_entry__ as g; g.build()'`")
+            handle = ctypes.CDLL(SAMPLER_PATH)
+            for name, (res, args) in _SAMPLER_SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _sampler = handle
+    return _sampler
+
+
+def check_sampler(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = sampler_lib().gnn_sampler_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
 
 
 def check(rc: int, what: str) -> None:

@@ -1,5 +1,6 @@
-"""In-tree build of libgnn_spmm.so (hipcc, gfx950). No JIT cache: the .so lives next to
-the package so it travels with the repository snapshot to the GPU box."""
+"""In-tree builds: libgnn_spmm.so (hipcc, gfx950) and libgnn_sampler.so (g++, host only).
+No JIT cache: the .so files live next to the package so they travel with the repository
+snapshot to the GPU box."""
 from __future__ import annotations
 
 import hashlib
@@ -42,5 +43,34 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+SAMPLER_SRCS = [os.path.join(HERE, "csrc", "sampler.cpp")]
+SAMPLER_HDRS = [os.path.join(REPO, "include", "gnn_sampler.h")]
+SAMPLER_OUT = os.path.join(HERE, "libgnn_sampler.so")
+
+
+def build_sampler(force: bool = False, verbose: bool = False) -> str:
+    h = hashlib.sha1()
+    for p in SAMPLER_SRCS + SAMPLER_HDRS:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    bid = h.hexdigest()[:12]
+    stamp = SAMPLER_OUT + ".buildid"
+    if not force and os.path.exists(SAMPLER_OUT) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == bid:
+                return SAMPLER_OUT
+    # x86-64-v2 (SSE4.2 + POPCNT), not -march=native: the GPU box's host CPU may differ
+    cmd = [os.environ.get("CXX", "g++"), "-O3", "-march=x86-64-v2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           f"-I{os.path.join(REPO, 'include')}", "-o", SAMPLER_OUT + ".tmp"] + SAMPLER_SRCS
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(SAMPLER_OUT + ".tmp", SAMPLER_OUT)
+    with open(stamp, "w") as f:
+        f.write(bid)
+    return SAMPLER_OUT
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))
+    print(build_sampler(force=True, verbose=True))

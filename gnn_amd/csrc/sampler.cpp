@@ -1,0 +1,322 @@
+// Native LADIES sampler (include/gnn_sampler.h): host C++ restatement of the per-batch
+// numpy/scipy work of ladies_sampler (reference sampler.py:90-160), bit-identical to it.
+//
+// The costs the numpy path pays per layer (csr row slicing, sp.linalg.norm, N-wide cumsum
+// per choice round, np.unique, scipy column indexing) become linear passes over the touched
+// rows plus O(#nonzero columns) work per choice round, on scratch arrays owned by the call —
+// so batches sample concurrently on host threads (ctypes releases the GIL).
+#include "gnn_sampler.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return -22;
+}
+
+// numpy's legacy MT19937 (RandomState): init_genrand seeding (mt19937_seed), the reference
+// generator, and random_sample's 53-bit double from two draws (mt19937_next_double).
+class MT19937 {
+ public:
+  explicit MT19937(uint32_t s) {
+    for (int i = 0; i < kN; ++i) {
+      key_[i] = s;
+      s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)i + 1u;
+    }
+    pos_ = kN;
+  }
+  uint32_t next32() {
+    if (pos_ == kN) gen();
+    uint32_t y = key_[pos_++];
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+  }
+  double next_double() {
+    const int32_t a = (int32_t)(next32() >> 5);
+    const int32_t b = (int32_t)(next32() >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+  }
+
+ private:
+  static constexpr int kN = 624, kM = 397;
+  static constexpr uint32_t kA = 0x9908b0dfu, kUp = 0x80000000u, kLo = 0x7fffffffu;
+  void gen() {
+    int i = 0;
+    uint32_t y;
+    for (; i < kN - kM; ++i) {
+      y = (key_[i] & kUp) | (key_[i + 1] & kLo);
+      key_[i] = key_[i + kM] ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    }
+    for (; i < kN - 1; ++i) {
+      y = (key_[i] & kUp) | (key_[i + 1] & kLo);
+      key_[i] = key_[i + (kM - kN)] ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    }
+    y = (key_[kN - 1] & kUp) | (key_[0] & kLo);
+    key_[kN - 1] = key_[kM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    pos_ = 0;
+  }
+  uint32_t key_[kN];
+  int pos_;
+};
+
+struct Layer {
+  bool present = false;
+  int64_t M = 0, K = 0, s_num = 0;
+  std::vector<int32_t> fullrowptr, rowptr, colidx;
+  std::vector<float> normfact;
+  std::vector<int64_t> sampled;
+};
+
+// RandomState.choice(N, size, p=p, replace=False) (numpy mtrand.pyx, legacy): rounds of
+// `rand(size - n_uniq)` draws, p of the already found entries zeroed, cdf = cumsum(p) /
+// cdf[-1], searchsorted(side='right'), de-duplicated in first-occurrence order.
+// cumsum over the zero entries adds +0.0 (exact) and searchsorted('right') never lands on a
+// zero-probability index, so both run over the ascending list of currently non-zero
+// entries `live` with identical results.
+void choice_without_replacement(MT19937& rng, const std::vector<int32_t>& cnt, double total,
+                                std::vector<int64_t> live, int64_t size, std::vector<uint8_t>& taken,
+                                std::vector<int64_t>& found) {
+  found.clear();
+  found.reserve((size_t)size);
+  std::vector<double> xs, cdf;
+  while ((int64_t)found.size() < size) {
+    const int64_t m = size - (int64_t)found.size();
+    xs.resize((size_t)m);
+    for (int64_t i = 0; i < m; ++i) xs[(size_t)i] = rng.next_double();
+    if (!found.empty()) {  // p[found] = 0: drop them from the live list
+      size_t w = 0;
+      for (size_t i = 0; i < live.size(); ++i)
+        if (!taken[(size_t)live[i]]) live[w++] = live[i];
+      live.resize(w);
+    }
+    cdf.resize(live.size());
+    double s = 0.0;
+    for (size_t i = 0; i < live.size(); ++i) {
+      s += (double)cnt[(size_t)live[i]] / total;
+      cdf[i] = s;
+    }
+    const double last = s;
+    for (size_t i = 0; i < cdf.size(); ++i) cdf[i] /= last;
+    for (int64_t i = 0; i < m; ++i) {
+      const size_t j = (size_t)(std::upper_bound(cdf.begin(), cdf.end(), xs[(size_t)i]) - cdf.begin());
+      // j == live.size() cannot happen for x < 1 = cdf.back(); guard anyway.
+      const int64_t v = live[j < live.size() ? j : live.size() - 1];
+      if (!taken[(size_t)v]) {
+        taken[(size_t)v] = 1;
+        found.push_back(v);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+struct gnn_ladies_result {
+  std::vector<Layer> layers;  // bottom-up
+  std::vector<int64_t> input_nodes;
+};
+
+extern "C" {
+
+const char* gnn_sampler_last_error(void) { return g_err.c_str(); }
+
+int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out) {
+  if (n < 0 || (n > 0 && !out)) return fail("gnn_mt19937_random_sample: bad arguments");
+  MT19937 rng(seed);
+  for (int64_t i = 0; i < n; ++i) out[i] = rng.next_double();
+  return 0;
+}
+
+int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                      const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                      const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
+  if (!out) return fail("gnn_ladies_sample: out is NULL");
+  *out = nullptr;
+  if (num_nodes <= 0 || num_nodes >= (int64_t)1 << 31) return fail("gnn_ladies_sample: num_nodes out of range");
+  if (!indptr || !indices) return fail("gnn_ladies_sample: NULL graph");
+  if (batch_size < 0 || (batch_size > 0 && !batch_nodes)) return fail("gnn_ladies_sample: bad batch");
+  if (num_layers < 0 || (num_layers > 0 && (!samp_num || !orders))) return fail("gnn_ladies_sample: bad layers");
+  const size_t N = (size_t)num_nodes;
+  for (int64_t i = 0; i < batch_size; ++i)
+    if (batch_nodes[i] < 0 || batch_nodes[i] >= num_nodes) return fail("gnn_ladies_sample: batch node out of range");
+  try {
+    std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
+    res->layers.resize((size_t)num_layers);
+    MT19937 rng(seed);
+    std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size);
+    std::vector<int32_t> cnt(N, 0);  // column nonzero counts of U (< nnz < 2^31)
+    std::vector<uint64_t> bits((N + 63) / 64);
+    std::vector<int32_t> wrank((N + 63) / 64);
+    std::vector<uint8_t> taken(N, 0), in_prev(N, 0);
+    std::vector<int64_t> live, found, after;
+    for (int32_t d = 0; d < num_layers; ++d) {
+      Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
+      if (orders[num_layers - 1 - d] == 0) continue;         // orders1 = orders[::-1]
+      L.present = true;
+      const int64_t M = (int64_t)prev.size();
+      // U = lap[prev, :] row pointers, column nonzero counts (ord-0 norm).
+      L.fullrowptr.resize((size_t)M + 1);
+      int64_t unnz = 0;
+      L.fullrowptr[0] = 0;
+      for (int64_t r = 0; r < M; ++r) {
+        const int64_t v = prev[(size_t)r];
+        const int64_t b = indptr[v], e = indptr[v + 1];
+        unnz += e - b;
+        if (unnz >= ((int64_t)1 << 31)) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
+        L.fullrowptr[(size_t)r + 1] = (int32_t)unnz;
+        if (data) {
+          for (int64_t k = b; k < e; ++k) cnt[(size_t)indices[k]] += (data[k] != 0.0f);
+        } else {
+          for (int64_t k = b; k < e; ++k) ++cnt[(size_t)indices[k]];
+        }
+      }
+      // p = pi / sum(pi): integer counts summed exactly, true division in double. `live`
+      // (ascending ids with p > 0) from one sequential scan instead of a sort.
+      int64_t isum = 0;
+      live.clear();
+      for (size_t c = 0; c < N; ++c) {
+        if (cnt[c]) {
+          isum += cnt[c];
+          live.push_back((int64_t)c);
+        }
+      }
+      if (isum == 0) {  // p = 0/0: numpy's choice raises "probabilities contain NaN"
+        return fail("gnn_ladies_sample: probabilities contain NaN (layer %d: no entries in U)", d);
+      }
+      const double total = (double)isum;
+      const int64_t s_num = std::min<int64_t>((int64_t)live.size(), samp_num[d]);
+      L.s_num = s_num;
+      choice_without_replacement(rng, cnt, total, live, s_num, taken, found);
+      // after = unique(concat(found, prev)), ascending.
+      after.assign(found.begin(), found.end());
+      after.insert(after.end(), prev.begin(), prev.end());
+      std::sort(after.begin(), after.end());
+      after.erase(std::unique(after.begin(), after.end()), after.end());
+      const int64_t K = (int64_t)after.size();
+      // Membership + renumbering of `after` as a bitmap with per-word rank prefixes
+      // (N/8 + N/16 bytes: L1/L2-resident, unlike an N-entry int32 map): the new column of
+      // c is rank[c / 64] + popcount(bits[c / 64] below bit c % 64).
+      std::fill(bits.begin(), bits.end(), 0ull);
+      for (int64_t a : after) bits[(size_t)a >> 6] |= 1ull << (a & 63);
+      int32_t acc = 0;
+      for (size_t wi = 0; wi < bits.size(); ++wi) {
+        wrank[wi] = acc;
+        acc += (int32_t)__builtin_popcountll(bits[wi]);
+      }
+      // adj = U[:, after]: per row, the entries whose column is in `after`, renumbered
+      // (branch-free compaction: ~10 % of the entries survive, unpredictably).
+      L.rowptr.resize((size_t)M + 1);
+      L.rowptr[0] = 0;
+      std::vector<int32_t> buf((size_t)unnz + 1);
+      int32_t* w = buf.data();
+      for (int64_t r = 0; r < M; ++r) {
+        const int64_t v = prev[(size_t)r];
+        for (int64_t k = indptr[v], e = indptr[v + 1]; k < e; ++k) {
+          const uint32_t c = (uint32_t)indices[k];
+          const uint64_t word = bits[c >> 6];
+          const uint32_t sh = c & 63u;
+          *w = wrank[c >> 6] + (int32_t)__builtin_popcountll(word & ((1ull << sh) - 1ull));
+          w += (word >> sh) & 1ull;
+        }
+        L.rowptr[(size_t)r + 1] = (int32_t)(w - buf.data());
+      }
+      L.colidx.assign(buf.data(), w);
+      // normfact = 1 / float32(clip(s_num * p[after], 1e-10, 1))  (float32 division)
+      L.normfact.resize((size_t)K);
+      const double sn = (double)s_num;
+      for (int64_t j = 0; j < K; ++j) {
+        double q = sn * ((double)cnt[(size_t)after[(size_t)j]] / total);
+        q = q < 1e-10 ? 1e-10 : (q > 1.0 ? 1.0 : q);  // NaN passes through, as np.clip
+        L.normfact[(size_t)j] = 1.0f / (float)q;
+      }
+      // sampled_nodes = where(isin(after, prev))
+      for (int64_t v : prev) in_prev[(size_t)v] = 1;
+      L.sampled.clear();
+      for (int64_t j = 0; j < K; ++j)
+        if (in_prev[(size_t)after[(size_t)j]]) L.sampled.push_back(j);
+      for (int64_t v : prev) in_prev[(size_t)v] = 0;
+      L.M = M;
+      L.K = K;
+      // reset scratch touched by this layer
+      for (int64_t c : live) cnt[(size_t)c] = 0;
+      for (int64_t v : found) taken[(size_t)v] = 0;
+      prev.swap(after);
+    }
+    res->input_nodes = prev;
+    *out = res.release();
+    return 0;
+  } catch (const std::bad_alloc&) {
+    return fail("gnn_ladies_sample: out of host memory");
+  }
+}
+
+int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dims[5]) {
+  if (!r || !dims || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_dims: bad args");
+  const Layer& L = r->layers[(size_t)layer];
+  dims[0] = L.M;
+  dims[1] = L.K;
+  dims[2] = (int64_t)L.colidx.size();
+  dims[3] = (int64_t)L.sampled.size();
+  dims[4] = L.s_num;
+  return L.present ? 0 : 1;
+}
+
+int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fullrowptr, int32_t* rowptr,
+                          int32_t* colidx, float* normfact, int64_t* sampled) {
+  if (!r || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_copy: bad args");
+  const Layer& L = r->layers[(size_t)layer];
+  auto cp = [](void* dst, const void* src, size_t bytes) {
+    if (dst && bytes) std::memcpy(dst, src, bytes);
+  };
+  cp(fullrowptr, L.fullrowptr.data(), L.fullrowptr.size() * 4);
+  cp(rowptr, L.rowptr.data(), L.rowptr.size() * 4);
+  cp(colidx, L.colidx.data(), L.colidx.size() * 4);
+  cp(normfact, L.normfact.data(), L.normfact.size() * 4);
+  cp(sampled, L.sampled.data(), L.sampled.size() * 8);
+  return 0;
+}
+
+int64_t gnn_ladies_num_input_nodes(const gnn_ladies_result* r) { return r ? (int64_t)r->input_nodes.size() : -1; }
+
+int gnn_ladies_input_nodes(const gnn_ladies_result* r, int64_t* out) {
+  if (!r || (!out && !r->input_nodes.empty())) return fail("gnn_ladies_input_nodes: bad args");
+  if (!r->input_nodes.empty()) std::memcpy(out, r->input_nodes.data(), r->input_nodes.size() * 8);
+  return 0;
+}
+
+void gnn_ladies_free(gnn_ladies_result* r) { delete r; }
+
+int gnn_host_gather_rows_f32(const float* src, int64_t ld_src, int64_t num_src_rows, const int64_t* idx, int64_t n,
+                             int64_t F, float* dst, int64_t ld_dst) {
+  if (n < 0 || F < 0 || F > ld_src || F > ld_dst || (n > 0 && (!src || !idx || !dst)))
+    return fail("gnn_host_gather_rows_f32: bad arguments");
+  for (int64_t i = 0; i < n; ++i)
+    if (idx[i] < 0 || idx[i] >= num_src_rows) return fail("gnn_host_gather_rows_f32: index %lld out of range", (long long)idx[i]);
+  for (int64_t i = 0; i < n; ++i) {
+    float* d = dst + i * ld_dst;
+    std::memcpy(d, src + idx[i] * ld_src, (size_t)F * sizeof(float));
+    if (ld_dst > F) std::memset(d + F, 0, (size_t)(ld_dst - F) * sizeof(float));
+  }
+  return 0;
+}
+
+}  // extern "C"

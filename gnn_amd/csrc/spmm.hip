@@ -890,7 +890,9 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
     const int g = atoi(eg);
     const char* en = getenv("GNN_SPMM_NJ");
     const int nj = en ? atoi(en) : 1;
-    if ((g == 16 || g == 32 || g == 64) && nj >= 1 && nj <= 8) {
+    const char* ev = getenv("GNN_SPMM_VW");
+    if (ev && atoi(ev) >= 1 && atoi(ev) < c.vw && (atoi(ev) & (atoi(ev) - 1)) == 0) c.vw = atoi(ev);
+    if ((g == 8 || g == 16 || g == 32 || g == 64) && nj >= 1 && nj <= 8) {
       c.g = g;
       c.nj = nj;
       c.tiles = (int)ceil_div(F, (int64_t)c.vw * g * nj);
@@ -933,6 +935,7 @@ MainFn main_by_g(int g, int nj) {
     case 64: return main_by_nj<VW, 64>(nj);
     case 32: return main_by_nj<VW, 32>(nj);
     case 16: return main_by_nj<VW, 16>(nj);
+    case 8: return main_by_nj<VW, 8>(nj);
     default: return nullptr;
   }
 }

@@ -54,16 +54,28 @@ class HostBatch:
     def nnz(self) -> int:
         return int(sum(l.colidx.size for l in self.layers if l is not None))
 
+    def pin(self) -> "HostBatch":
+        """Copy the arrays the GPU needs into pinned host tensors (done by the batch producer
+        thread, so the training thread only issues asynchronous copies)."""
+        if "pinned" not in self.extra:
+            pin = torch.cuda.is_available()
+            t = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))
+            p = lambda x: x.pin_memory() if pin else x
+            layers = [None if L is None else (p(t(L.fullrowptr)), p(t(L.rowptr)), p(t(L.colidx)), p(t(L.normfact)))
+                      for L in self.layers]
+            sampled = [p(t(s, np.int64)) for s in self.sampled_nodes]
+            self.extra["pinned"] = (layers, sampled, p(t(self.labels)))
+        return self
+
     def to_device(self, device, with_coo: bool = True, build: bool = True):
         """Materialise on the GPU (H2D of the CSR pieces, labels, sampled_nodes) and, unless
         build=False, run the operand builder. Returns a DeviceBatch."""
         dev = torch.device(device)
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)
-        raw = [None if L is None else (t(L.fullrowptr), t(L.rowptr), t(L.colidx), t(L.normfact), L.shape)
-               for L in self.layers]
-        sampled = [torch.from_numpy(np.asarray(s, dtype=np.int64)).to(dev, non_blocking=True) for s in self.sampled_nodes]
-        labels = torch.from_numpy(self.labels).to(dev, non_blocking=True)
-        db = DeviceBatch(self, raw, None, sampled, labels)
+        layers, sampled, labels = self.pin().extra["pinned"]
+        d = lambda x: x.to(dev, non_blocking=True)
+        raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape)
+               for P, L in zip(layers, self.layers)]
+        db = DeviceBatch(self, raw, None, [d(s) for s in sampled], d(labels))
         if build:
             db.build_operands(with_coo=with_coo)
         return db
@@ -104,10 +116,119 @@ def column_nnz_counts(U: sp.csr_matrix, num_nodes: int) -> np.ndarray:
     return np.bincount(idx, minlength=num_nodes).astype(np.int64)
 
 
-def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix: sp.csr_matrix, labels_full,
+class NativeGraph:
+    """The lap matrix as the native sampler reads it: canonical CSR (sorted, duplicate-free
+    rows — what sp.linalg.norm makes of U in place, sampler.py:117), int64 indptr, int32
+    indices, float32 data. Built once per graph; shared read-only by sampler threads."""
+
+    def __init__(self, lap: sp.csr_matrix):
+        self.src = lap  # the caller's matrix (cache key; kept alive so its id stays unique)
+        if not sp.isspmatrix_csr(lap):
+            lap = sp.csr_matrix(lap)
+        if not lap.has_canonical_format:
+            lap = lap.copy()
+            lap.sum_duplicates()
+        self.num_nodes = int(lap.shape[0])
+        if lap.shape[1] != lap.shape[0]:
+            raise ValueError("lap_matrix must be square")
+        self.indptr = np.ascontiguousarray(lap.indptr, dtype=np.int64)
+        self.indices = np.ascontiguousarray(lap.indices, dtype=np.int32)
+        data = np.asarray(lap.data)
+        # data == 0 entries are structure but not counted (ord-0 norm); skip the array if none
+        self.data = None if np.all(data != 0) else np.ascontiguousarray(data, dtype=np.float32)
+        self.lap = lap
+
+
+_native_graphs: "dict[int, NativeGraph]" = {}
+
+
+def native_graph(lap) -> NativeGraph:
+    if isinstance(lap, NativeGraph):
+        return lap
+    g = _native_graphs.get(id(lap))
+    if g is None or g.src is not lap:
+        g = NativeGraph(lap)
+        _native_graphs.clear()  # one graph per process in practice; do not pin old ones
+        _native_graphs[id(lap)] = g
+    return g
+
+
+def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders):
+    """Run gnn_ladies_sample and copy the result out: (layers, sampled_nodes, input_nodes)."""
+    import ctypes
+
+    from . import _lib
+
+    L = _lib.sampler_lib()
+    bn = np.ascontiguousarray(batch_nodes, dtype=np.int64)
+    nl = len(orders)
+    sn = np.ascontiguousarray([int(samp_num_list[d]) for d in range(nl)], dtype=np.int64)
+    od = np.ascontiguousarray(orders, dtype=np.int32)
+    ptr = lambda a: None if a is None else a.ctypes.data
+    h = ctypes.c_void_p()
+    _lib.check_sampler(L.gnn_ladies_sample(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), graph.num_nodes,
+                                           ptr(bn), bn.size, ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF,
+                                           ctypes.byref(h)), "gnn_ladies_sample")
+    # Outputs land straight in pinned host tensors (when a GPU is present): HostBatch.pin()
+    # then has nothing left to copy and the H2D copies can be asynchronous.
+    pin = torch.cuda.is_available()
+    pinned_layers, pinned_sampled = [], []
+
+    def buf(n, dt):
+        t = torch.empty(int(n), dtype=dt, pin_memory=pin)
+        return t, t.numpy()
+
+    try:
+        layers: List[Optional[HostLayer]] = []
+        sampled: List[np.ndarray] = []
+        dims = (ctypes.c_int64 * 5)()
+        for li in range(nl):
+            absent = L.gnn_ladies_layer_dims(h, li, dims)
+            if absent:
+                layers.append(None)
+                sampled.append(np.zeros(0, dtype=np.int64))
+                pinned_layers.append(None)
+                pinned_sampled.append(buf(0, torch.int64)[0])
+                continue
+            M, K, nnz, ns = dims[0], dims[1], dims[2], dims[3]
+            (tfr, fr), (trp, rp), (tci, ci) = buf(M + 1, torch.int32), buf(M + 1, torch.int32), buf(nnz, torch.int32)
+            (tnf, nf), (tsa, sa) = buf(K, torch.float32), buf(ns, torch.int64)
+            pinned_layers.append((tfr, trp, tci, tnf))
+            pinned_sampled.append(tsa)
+            _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, ptr(fr), ptr(rp), ptr(ci), ptr(nf), ptr(sa)),
+                               "gnn_ladies_layer_copy")
+            layers.append(HostLayer(fullrowptr=fr, rowptr=rp, colidx=ci, normfact=nf, shape=(int(M), int(K))))
+            sampled.append(sa)
+        inp = np.empty(L.gnn_ladies_num_input_nodes(h), np.int64)
+        _lib.check_sampler(L.gnn_ladies_input_nodes(h, ptr(inp)), "gnn_ladies_input_nodes")
+    finally:
+        L.gnn_ladies_free(h)
+    return layers, sampled, inp, (pinned_layers, pinned_sampled)
+
+
+def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
                        orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
-                       skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,)) -> HostBatch:
-    """sampler.py:90-160 without the device work."""
+                       skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
+                       native: bool = True) -> HostBatch:
+    """sampler.py:90-160 without the device work.
+
+    native=True runs the C++ sampler (libgnn_sampler.so, bit-identical; releases the GIL, so
+    batches sample concurrently on threads); native=False (and scale_factor > 1, a branch the
+    reference never reaches) runs the numpy restatement below."""
+    batch_nodes = np.asarray(batch_nodes)
+    if native and not scale_factor > 1:
+        g = native_graph(lap_matrix)
+        if g.num_nodes != num_nodes:
+            raise ValueError("num_nodes does not match lap_matrix")
+        layers, sampled_nodes, previous_nodes, pinned = _native_layers(seed, batch_nodes, samp_num_list, g,
+                                                                       list(orders))
+        hb = _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,
+                           idx_of_nodes_on_device, devices, seed)
+        lab = torch.from_numpy(hb.labels)
+        hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        return hb
+    if isinstance(lap_matrix, NativeGraph):
+        lap_matrix = lap_matrix.lap
     np.random.seed(seed)
     batch_nodes = np.asarray(batch_nodes)
     previous_nodes = batch_nodes
@@ -149,7 +270,13 @@ def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix: 
         previous_nodes = after_nodes
     layers.reverse()
     sampled_nodes.reverse()
+    return _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,
+                         idx_of_nodes_on_device, devices, seed)
 
+
+def _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,
+                  idx_of_nodes_on_device, devices, seed) -> HostBatch:
+    """Feature-placement masks and labels of a sampled batch (sampler.py:150-160)."""
     input_nodes_devices = device_id_of_nodes[previous_nodes]
     input_nodes_mask_on_cpu = input_nodes_devices == -1
     nodes_idx_on_cpu = previous_nodes[input_nodes_mask_on_cpu]

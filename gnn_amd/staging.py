@@ -43,18 +43,26 @@ class FeatureStore:
         self.rank = rank
         self.F = int(feat_data.shape[1])
         self.ld = padded_ld(self.F)
-        self.host = feat_data.pin_memory() if pin_host else feat_data
+        self.host = feat_data.pin_memory() if pin_host else feat_data.contiguous()
         idx = torch.from_numpy(np.asarray(buffer_nodes, dtype=np.int64))
         buf = torch.zeros((len(idx), self.ld), dtype=torch.float32)
         buf[:, : self.F] = feat_data[idx]
         self.gpu_buffer = buf.to(self.device)  # (k x ld), row i = node buffer_nodes[i]
 
     def host_rows_pinned(self, node_ids: np.ndarray) -> torch.Tensor:
-        """Host gather of non-buffered rows into a pinned (n x ld) tensor (zero padding)."""
-        n = len(node_ids)
-        out = torch.zeros((n, self.ld), dtype=torch.float32).pin_memory()
+        """Host gather of non-buffered rows into a pinned (n x ld) tensor (zero padding):
+        one native row-copy loop (gnn_host_gather_rows_f32, GIL released) straight into
+        the pinned buffer, so sampler worker threads stage concurrently."""
+        from . import _lib
+
+        idx = np.ascontiguousarray(node_ids, dtype=np.int64)
+        n = len(idx)
+        out = torch.empty((n, self.ld), dtype=torch.float32, pin_memory=torch.cuda.is_available())
         if n:
-            out[:, : self.F] = self.host[torch.from_numpy(np.asarray(node_ids, dtype=np.int64))]
+            host = self.host
+            _lib.check_sampler(_lib.sampler_lib().gnn_host_gather_rows_f32(
+                host.data_ptr(), host.stride(0), host.shape[0], idx.ctypes.data, n, self.F, out.data_ptr(), self.ld),
+                "gnn_host_gather_rows_f32")
         return out
 
 
@@ -87,7 +95,8 @@ def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devic
         else:
             peer_pos.append(np.flatnonzero(masks[j]).astype(np.int64))
             peer_src.append(np.asarray(idxs[j], dtype=np.int64))
-    pin = tuple(torch.from_numpy(a).pin_memory() for a in (own_pos, own_src, host_pos))
+    cuda = torch.cuda.is_available()
+    pin = tuple(torch.from_numpy(a).pin_memory() if cuda else torch.from_numpy(a) for a in (own_pos, own_src, host_pos))
     return StagePlan(host_batch.num_input_nodes, own_pos, own_src, host_pos, host_rows, peer_pos, peer_src, pin)
 
 

@@ -1,0 +1,73 @@
+/*
+ * gnn_sampler.h — native LADIES layer-wise sampler (host C++, libgnn_sampler.so).
+ *
+ * Replaces the per-batch numpy/scipy work of ladies_sampler (sampler.py:90-160): for each
+ * layer, top-down, U = lap[previous, :] (sampler.py:112), column nonzero counts of U
+ * (sp.linalg.norm(U, ord=0, axis=0), :117), p = counts / sum (:122),
+ * s_num = min(#(p > 0), samp_num) (:126), np.random.choice(N, s_num, p=p, replace=False)
+ * under np.random.seed(seed) (:96, :128 — numpy's legacy MT19937 stream and its
+ * without-replacement loop restated exactly), after = unique(sampled ∪ previous) (:131),
+ * the sub-graph U[:, after] as CSR (:133-136, int32 columns instead of int16),
+ * normfact = 1 / float32(clip(s_num * p[after], 1e-10, 1)) (:137) and
+ * sampled_nodes = positions of previous in after (:143).
+ * Results are bit-identical to the numpy path (tests/test_sampler_native.py).
+ *
+ * The graph is CSR with sorted, duplicate-free column indices per row (scipy canonical
+ * format: the reference's sp.linalg.norm canonicalises U in place before U[:, after]).
+ * `data` may be NULL (every stored entry non-zero); otherwise entries equal to 0 are kept
+ * in the structure but not counted, as sp.linalg.norm(ord=0) does.
+ *
+ * Thread-safe: independent calls may run concurrently (each owns its scratch). Returns 0 or
+ * a non-zero status; text via gnn_sampler_last_error() (thread-local).
+ */
+#ifndef GNN_SAMPLER_H
+#define GNN_SAMPLER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gnn_ladies_result gnn_ladies_result;
+
+const char* gnn_sampler_last_error(void);
+
+/* Sample one mini-batch. orders[num_layers] bottom-up as the reference's `orders`;
+ * samp_num[num_layers] indexed top-down as samp_num_list[d] (sampler.py:124). A layer with
+ * order 0 yields no sub-graph (sampler.py:107-110). On success *out owns the result. */
+int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                      const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                      const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
+
+/* dims of layer `layer` (bottom-up, as the returned adjs): {M, K, nnz, n_sampled, s_num}.
+ * Returns 1 if the layer has order 0 (no sub-graph), 0 otherwise. */
+int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dims[5]);
+
+/* Copy layer arrays out: fullrowptr int32[M+1] (indptr of U), rowptr int32[M+1] (indptr of
+ * U[:, after]), colidx int32[nnz], normfact float32[K], sampled int64[n_sampled]. Any
+ * pointer may be NULL to skip that array. */
+int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fullrowptr, int32_t* rowptr,
+                          int32_t* colidx, float* normfact, int64_t* sampled);
+
+/* The layer-0 input node ids (the last `after`, sorted). */
+int64_t gnn_ladies_num_input_nodes(const gnn_ladies_result* r);
+int gnn_ladies_input_nodes(const gnn_ladies_result* r, int64_t* out);
+
+void gnn_ladies_free(gnn_ladies_result* r);
+
+/* Host half of the layer-0 feature staging (main.py:134, `feat_data[idx_cpu]`): copy rows
+ * src[idx[i], 0:F] into dst row i (stride ld_dst, columns [F, ld_dst) zeroed) — typically a
+ * pinned buffer that one hipMemcpyAsync then moves to the GPU. */
+int gnn_host_gather_rows_f32(const float* src, int64_t ld_src, int64_t num_src_rows, const int64_t* idx, int64_t n,
+                             int64_t F, float* dst, int64_t ld_dst);
+
+/* numpy legacy RandomState(seed).random_sample(n) — exposed for the RNG-stream tests. */
+int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNN_SAMPLER_H */

@@ -11,9 +11,9 @@ from gnn_amd import _lib
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared():
+def _declared(headers=("gnn_spmm.h", "gnn_layers.h")):
     txt = ""
-    for h in ("gnn_spmm.h", "gnn_layers.h"):
+    for h in headers:
         with open(os.path.join(REPO, "include", h)) as f:
             txt += f.read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
@@ -27,6 +27,28 @@ def test_library_exports_header_symbols():
     for name in decl:
         assert hasattr(L, name), f"{name} declared in gnn_spmm.h but not exported"
     assert set(decl) == set(_lib.EXPORTED_SYMBOLS)
+
+
+def test_sampler_library_exports_header_symbols():
+    L = _lib.sampler_lib()
+    decl = _declared(("gnn_sampler.h",))
+    for name in decl:
+        assert hasattr(L, name), f"{name} declared in gnn_sampler.h but not exported"
+    assert set(decl) == set(_lib.SAMPLER_EXPORTED_SYMBOLS)
+
+
+def test_host_gather_rows():
+    import numpy as np
+
+    L = _lib.sampler_lib()
+    src = np.arange(50 * 7, dtype=np.float32).reshape(50, 7)
+    idx = np.array([3, 0, 49, 3], np.int64)
+    dst = np.full((4, 8), -1.0, np.float32)
+    _lib.check_sampler(L.gnn_host_gather_rows_f32(src.ctypes.data, 7, 50, idx.ctypes.data, 4, 7, dst.ctypes.data, 8),
+                       "gather")
+    assert np.array_equal(dst[:, :7], src[idx]) and np.all(dst[:, 7] == 0)
+    bad = np.array([50], np.int64)
+    assert L.gnn_host_gather_rows_f32(src.ctypes.data, 7, 50, bad.ctypes.data, 1, 7, dst.ctypes.data, 8) != 0
 
 
 def test_version_and_error_strings():

@@ -1,5 +1,6 @@
 """CPU: host sampler and placement restatements vs the reference's goldens (bit-exact)."""
 import numpy as np
+import pytest
 import scipy.sparse as sp
 
 from gnn_amd import placement, sampler
@@ -50,14 +51,16 @@ def test_placement_cache_roundtrip(golden, tmp_path):
     assert np.array_equal(a.idx_of_nodes_on_device_group[0], b.idx_of_nodes_on_device_group[0])
 
 
-def test_ladies_matches_reference(golden):
+@pytest.mark.parametrize("native", [True, False])
+def test_ladies_matches_reference(golden, native):
     _, lap, labels, _, N = _graph(golden)
     z = golden("ladies_tiny.npz")
     pl = golden("placement_tiny.npz")
     for c in range(4):
         samp, bs, seed, ndev = (int(v) for v in z[f"c{c}_cfg"])
         hb = sampler.ladies_sample_host(seed, z[f"c{c}_batch"], np.array([samp] * 5), N, lap, labels, [1, 1, 1],
-                                        pl[f"n{ndev}_dev0"], pl[f"n{ndev}_idx"], None, 1.0, list(range(ndev)))
+                                        pl[f"n{ndev}_dev0"], pl[f"n{ndev}_idx"], None, 1.0, list(range(ndev)),
+                                        native=native)
         for li in range(3):  # recorded top-down; hb.layers bottom-up
             L = hb.layers[2 - li]
             p = f"c{c}_call{li}_"
