@@ -128,6 +128,142 @@ void choice_without_replacement(MT19937& rng, const std::vector<int32_t>& cnt, d
   }
 }
 
+struct Graph {
+  const int64_t* indptr;
+  const int32_t* indices;
+  const float* data;
+  size_t N;
+};
+
+// Per-call scratch (N-sized arrays) and the steps both samplers are built from.
+class Work {
+ public:
+  explicit Work(const Graph& g) : g_(g), cnt(g.N, 0), bits((g.N + 63) / 64), wrank((g.N + 63) / 64),
+                                  taken(g.N, 0), in_prev(g.N, 0) {}
+
+  // Row pointers of U = lap[rows, :] into fullrowptr; returns nnz(U) or -1 if >= 2^31.
+  int64_t row_pointers(const std::vector<int64_t>& rows, std::vector<int32_t>& fullrowptr) const {
+    fullrowptr.resize(rows.size() + 1);
+    fullrowptr[0] = 0;
+    int64_t unnz = 0;
+    for (size_t r = 0; r < rows.size(); ++r) {
+      unnz += g_.indptr[rows[r] + 1] - g_.indptr[rows[r]];
+      if (unnz >= ((int64_t)1 << 31)) return -1;
+      fullrowptr[r + 1] = (int32_t)unnz;
+    }
+    return unnz;
+  }
+
+  // Column nonzero counts of U = lap[rows, :] (sp.linalg.norm(U, ord=0, axis=0)); `live` =
+  // ascending columns with a non-zero count (one sequential scan, no sort); returns the sum.
+  int64_t count_columns(const std::vector<int64_t>& rows) {
+    for (int64_t v : rows) {
+      const int64_t b = g_.indptr[v], e = g_.indptr[v + 1];
+      if (g_.data) {
+        for (int64_t k = b; k < e; ++k) cnt[(size_t)g_.indices[k]] += (g_.data[k] != 0.0f);
+      } else {
+        for (int64_t k = b; k < e; ++k) ++cnt[(size_t)g_.indices[k]];
+      }
+    }
+    int64_t isum = 0;
+    live.clear();
+    for (size_t c = 0; c < g_.N; ++c) {
+      if (cnt[c]) {
+        isum += cnt[c];
+        live.push_back((int64_t)c);
+      }
+    }
+    return isum;
+  }
+
+  void clear_counts() {
+    for (int64_t c : live) cnt[(size_t)c] = 0;
+  }
+
+  // after = unique(concat(found, prev)), ascending; then the membership bitmap of `after`
+  // with per-word rank prefixes (N/8 + N/16 bytes: L1/L2-resident, unlike an N-entry int32
+  // map): the new column of c is rank[c / 64] + popcount(bits[c / 64] below bit c % 64).
+  void make_after(const std::vector<int64_t>& prev, std::vector<int64_t>& after) {
+    after.assign(found.begin(), found.end());
+    after.insert(after.end(), prev.begin(), prev.end());
+    std::sort(after.begin(), after.end());
+    after.erase(std::unique(after.begin(), after.end()), after.end());
+    for (int64_t v : found) taken[(size_t)v] = 0;
+    set_columns(after);
+  }
+
+  void set_columns(const std::vector<int64_t>& cols) {
+    std::fill(bits.begin(), bits.end(), 0ull);
+    for (int64_t a : cols) bits[(size_t)a >> 6] |= 1ull << (a & 63);
+    int32_t acc = 0;
+    for (size_t wi = 0; wi < bits.size(); ++wi) {
+      wrank[wi] = acc;
+      acc += (int32_t)__builtin_popcountll(bits[wi]);
+    }
+  }
+
+  // adj = lap[rows, :][:, cols] (scipy column indexing with sorted unique cols): per row,
+  // the entries whose column is a member, renumbered (branch-free compaction).
+  void extract(const std::vector<int64_t>& rows, int64_t unnz, Layer& L) const {
+    L.rowptr.resize(rows.size() + 1);
+    L.rowptr[0] = 0;
+    std::vector<int32_t> buf((size_t)unnz + 1);
+    int32_t* w = buf.data();
+    for (size_t r = 0; r < rows.size(); ++r) {
+      const int64_t v = rows[r];
+      for (int64_t k = g_.indptr[v], e = g_.indptr[v + 1]; k < e; ++k) {
+        const uint32_t c = (uint32_t)g_.indices[k];
+        const uint64_t word = bits[c >> 6];
+        const uint32_t sh = c & 63u;
+        *w = wrank[c >> 6] + (int32_t)__builtin_popcountll(word & ((1ull << sh) - 1ull));
+        w += (word >> sh) & 1ull;
+      }
+      L.rowptr[r + 1] = (int32_t)(w - buf.data());
+    }
+    L.colidx.assign(buf.data(), w);
+  }
+
+  // normfact = 1 / float32(clip(s_num * p[cols], 1e-10, 1))  (sampler.py:137: float32 division)
+  void normfact(const std::vector<int64_t>& cols, double total, int64_t s_num, Layer& L) const {
+    L.normfact.resize(cols.size());
+    const double sn = (double)s_num;
+    for (size_t j = 0; j < cols.size(); ++j) {
+      double q = sn * ((double)cnt[(size_t)cols[j]] / total);
+      q = q < 1e-10 ? 1e-10 : (q > 1.0 ? 1.0 : q);  // NaN passes through, as np.clip
+      L.normfact[j] = 1.0f / (float)q;
+    }
+  }
+
+  // sampled_nodes = where(isin(after, prev))
+  void positions(const std::vector<int64_t>& after, const std::vector<int64_t>& prev, Layer& L) {
+    for (int64_t v : prev) in_prev[(size_t)v] = 1;
+    L.sampled.clear();
+    for (size_t j = 0; j < after.size(); ++j)
+      if (in_prev[(size_t)after[j]]) L.sampled.push_back((int64_t)j);
+    for (int64_t v : prev) in_prev[(size_t)v] = 0;
+  }
+
+  const Graph& g_;
+  std::vector<int32_t> cnt;  // column nonzero counts of U (< nnz < 2^31)
+  std::vector<uint64_t> bits;
+  std::vector<int32_t> wrank;
+  std::vector<uint8_t> taken, in_prev;
+  std::vector<int64_t> live, found;
+};
+
+int check_inputs(const char* who, const int64_t* indptr, const int32_t* indices, int64_t num_nodes,
+                 const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num, const int32_t* orders,
+                 int32_t num_layers, void* out) {
+  if (!out) return fail("%s: out is NULL", who);
+  if (num_nodes <= 0 || num_nodes >= (int64_t)1 << 31) return fail("%s: num_nodes out of range", who);
+  if (!indptr || !indices) return fail("%s: NULL graph", who);
+  if (batch_size < 0 || (batch_size > 0 && !batch_nodes)) return fail("%s: bad batch", who);
+  if (num_layers < 0 || (num_layers > 0 && (!samp_num || !orders))) return fail("%s: bad layers", who);
+  for (int64_t i = 0; i < batch_size; ++i)
+    if (batch_nodes[i] < 0 || batch_nodes[i] >= num_nodes) return fail("%s: batch node out of range", who);
+  return 0;
+}
+
 }  // namespace
 
 struct gnn_ladies_result {
@@ -149,116 +285,37 @@ int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out) {
 int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
-  if (!out) return fail("gnn_ladies_sample: out is NULL");
+  if (int rc = check_inputs("gnn_ladies_sample", indptr, indices, num_nodes, batch_nodes, batch_size, samp_num,
+                            orders, num_layers, out))
+    return rc;
   *out = nullptr;
-  if (num_nodes <= 0 || num_nodes >= (int64_t)1 << 31) return fail("gnn_ladies_sample: num_nodes out of range");
-  if (!indptr || !indices) return fail("gnn_ladies_sample: NULL graph");
-  if (batch_size < 0 || (batch_size > 0 && !batch_nodes)) return fail("gnn_ladies_sample: bad batch");
-  if (num_layers < 0 || (num_layers > 0 && (!samp_num || !orders))) return fail("gnn_ladies_sample: bad layers");
-  const size_t N = (size_t)num_nodes;
-  for (int64_t i = 0; i < batch_size; ++i)
-    if (batch_nodes[i] < 0 || batch_nodes[i] >= num_nodes) return fail("gnn_ladies_sample: batch node out of range");
   try {
+    const Graph g{indptr, indices, data, (size_t)num_nodes};
+    Work w(g);
     std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
     res->layers.resize((size_t)num_layers);
     MT19937 rng(seed);
-    std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size);
-    std::vector<int32_t> cnt(N, 0);  // column nonzero counts of U (< nnz < 2^31)
-    std::vector<uint64_t> bits((N + 63) / 64);
-    std::vector<int32_t> wrank((N + 63) / 64);
-    std::vector<uint8_t> taken(N, 0), in_prev(N, 0);
-    std::vector<int64_t> live, found, after;
+    std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size), after;
     for (int32_t d = 0; d < num_layers; ++d) {
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
       if (orders[num_layers - 1 - d] == 0) continue;         // orders1 = orders[::-1]
       L.present = true;
-      const int64_t M = (int64_t)prev.size();
-      // U = lap[prev, :] row pointers, column nonzero counts (ord-0 norm).
-      L.fullrowptr.resize((size_t)M + 1);
-      int64_t unnz = 0;
-      L.fullrowptr[0] = 0;
-      for (int64_t r = 0; r < M; ++r) {
-        const int64_t v = prev[(size_t)r];
-        const int64_t b = indptr[v], e = indptr[v + 1];
-        unnz += e - b;
-        if (unnz >= ((int64_t)1 << 31)) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
-        L.fullrowptr[(size_t)r + 1] = (int32_t)unnz;
-        if (data) {
-          for (int64_t k = b; k < e; ++k) cnt[(size_t)indices[k]] += (data[k] != 0.0f);
-        } else {
-          for (int64_t k = b; k < e; ++k) ++cnt[(size_t)indices[k]];
-        }
-      }
-      // p = pi / sum(pi): integer counts summed exactly, true division in double. `live`
-      // (ascending ids with p > 0) from one sequential scan instead of a sort.
-      int64_t isum = 0;
-      live.clear();
-      for (size_t c = 0; c < N; ++c) {
-        if (cnt[c]) {
-          isum += cnt[c];
-          live.push_back((int64_t)c);
-        }
-      }
-      if (isum == 0) {  // p = 0/0: numpy's choice raises "probabilities contain NaN"
+      const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
+      if (unnz < 0) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
+      const int64_t isum = w.count_columns(prev);  // p = pi / sum(pi): exact integer sum
+      if (isum == 0)  // p = 0/0: numpy's choice raises "probabilities contain NaN"
         return fail("gnn_ladies_sample: probabilities contain NaN (layer %d: no entries in U)", d);
-      }
       const double total = (double)isum;
-      const int64_t s_num = std::min<int64_t>((int64_t)live.size(), samp_num[d]);
+      const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[d]);
       L.s_num = s_num;
-      choice_without_replacement(rng, cnt, total, live, s_num, taken, found);
-      // after = unique(concat(found, prev)), ascending.
-      after.assign(found.begin(), found.end());
-      after.insert(after.end(), prev.begin(), prev.end());
-      std::sort(after.begin(), after.end());
-      after.erase(std::unique(after.begin(), after.end()), after.end());
-      const int64_t K = (int64_t)after.size();
-      // Membership + renumbering of `after` as a bitmap with per-word rank prefixes
-      // (N/8 + N/16 bytes: L1/L2-resident, unlike an N-entry int32 map): the new column of
-      // c is rank[c / 64] + popcount(bits[c / 64] below bit c % 64).
-      std::fill(bits.begin(), bits.end(), 0ull);
-      for (int64_t a : after) bits[(size_t)a >> 6] |= 1ull << (a & 63);
-      int32_t acc = 0;
-      for (size_t wi = 0; wi < bits.size(); ++wi) {
-        wrank[wi] = acc;
-        acc += (int32_t)__builtin_popcountll(bits[wi]);
-      }
-      // adj = U[:, after]: per row, the entries whose column is in `after`, renumbered
-      // (branch-free compaction: ~10 % of the entries survive, unpredictably).
-      L.rowptr.resize((size_t)M + 1);
-      L.rowptr[0] = 0;
-      std::vector<int32_t> buf((size_t)unnz + 1);
-      int32_t* w = buf.data();
-      for (int64_t r = 0; r < M; ++r) {
-        const int64_t v = prev[(size_t)r];
-        for (int64_t k = indptr[v], e = indptr[v + 1]; k < e; ++k) {
-          const uint32_t c = (uint32_t)indices[k];
-          const uint64_t word = bits[c >> 6];
-          const uint32_t sh = c & 63u;
-          *w = wrank[c >> 6] + (int32_t)__builtin_popcountll(word & ((1ull << sh) - 1ull));
-          w += (word >> sh) & 1ull;
-        }
-        L.rowptr[(size_t)r + 1] = (int32_t)(w - buf.data());
-      }
-      L.colidx.assign(buf.data(), w);
-      // normfact = 1 / float32(clip(s_num * p[after], 1e-10, 1))  (float32 division)
-      L.normfact.resize((size_t)K);
-      const double sn = (double)s_num;
-      for (int64_t j = 0; j < K; ++j) {
-        double q = sn * ((double)cnt[(size_t)after[(size_t)j]] / total);
-        q = q < 1e-10 ? 1e-10 : (q > 1.0 ? 1.0 : q);  // NaN passes through, as np.clip
-        L.normfact[(size_t)j] = 1.0f / (float)q;
-      }
-      // sampled_nodes = where(isin(after, prev))
-      for (int64_t v : prev) in_prev[(size_t)v] = 1;
-      L.sampled.clear();
-      for (int64_t j = 0; j < K; ++j)
-        if (in_prev[(size_t)after[(size_t)j]]) L.sampled.push_back(j);
-      for (int64_t v : prev) in_prev[(size_t)v] = 0;
-      L.M = M;
-      L.K = K;
-      // reset scratch touched by this layer
-      for (int64_t c : live) cnt[(size_t)c] = 0;
-      for (int64_t v : found) taken[(size_t)v] = 0;
+      choice_without_replacement(rng, w.cnt, total, w.live, s_num, w.taken, w.found);
+      w.make_after(prev, after);
+      w.extract(prev, unnz, L);
+      w.normfact(after, total, s_num, L);
+      w.positions(after, prev, L);
+      L.M = (int64_t)prev.size();
+      L.K = (int64_t)after.size();
+      w.clear_counts();
       prev.swap(after);
     }
     res->input_nodes = prev;
@@ -266,6 +323,69 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_ladies_sample: out of host memory");
+  }
+}
+
+int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                        const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                        const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
+  if (int rc = check_inputs("gnn_subgraph_sample", indptr, indices, num_nodes, batch_nodes, batch_size, samp_num,
+                            orders, num_layers, out))
+    return rc;
+  *out = nullptr;
+  try {
+    const Graph g{indptr, indices, data, (size_t)num_nodes};
+    Work w(g);
+    std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
+    res->layers.resize((size_t)num_layers);
+    MT19937 rng(seed);
+    const std::vector<int64_t> batch(batch_nodes, batch_nodes + batch_size);
+    std::vector<int64_t> after;
+    // One importance draw from the batch's neighbourhood (sampler.py:19-38) ...
+    Layer first;
+    const int64_t unnz = w.row_pointers(batch, first.fullrowptr);
+    if (unnz < 0) return fail("gnn_subgraph_sample: sub-graph nnz >= 2^31");
+    const int64_t isum = w.count_columns(batch);
+    if (isum == 0) return fail("gnn_subgraph_sample: probabilities contain NaN (no entries in U)");
+    const double total = (double)isum;
+    const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[0]);
+    choice_without_replacement(rng, w.cnt, total, w.live, s_num, w.taken, w.found);
+    w.make_after(batch, after);
+    // ... the top-most layer with a non-zero order takes U[:, after] (sampler.py:42-53) ...
+    int32_t d = 0;
+    for (; d < num_layers; ++d) {
+      if (orders[num_layers - 1 - d] == 0) continue;
+      Layer& L = res->layers[(size_t)(num_layers - 1 - d)];
+      L = std::move(first);
+      L.present = true;
+      L.s_num = s_num;
+      w.extract(batch, unnz, L);
+      w.normfact(after, total, s_num, L);
+      w.positions(after, batch, L);
+      L.M = (int64_t)batch.size();
+      L.K = (int64_t)after.size();
+      ++d;
+      break;
+    }
+    // ... and EVERY layer below it (whatever its order, sampler.py:55-69) the square
+    // sub-graph lap[after, :][:, after], same normfact, sampled_nodes = arange(len(after)).
+    for (; d < num_layers; ++d) {
+      Layer& L = res->layers[(size_t)(num_layers - 1 - d)];
+      L.present = true;
+      L.s_num = s_num;
+      const int64_t n2 = w.row_pointers(after, L.fullrowptr);
+      if (n2 < 0) return fail("gnn_subgraph_sample: sub-graph nnz >= 2^31");
+      w.extract(after, n2, L);
+      w.normfact(after, total, s_num, L);
+      L.sampled.resize(after.size());
+      for (size_t j = 0; j < after.size(); ++j) L.sampled[j] = (int64_t)j;
+      L.M = L.K = (int64_t)after.size();
+    }
+    res->input_nodes = after;
+    *out = res.release();
+    return 0;
+  } catch (const std::bad_alloc&) {
+    return fail("gnn_subgraph_sample: out of host memory");
   }
 }
 

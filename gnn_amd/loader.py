@@ -77,7 +77,10 @@ class BatchLoader:
     def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
-                 seed: int = 0, devices=None):
+                 seed: int = 0, devices=None, kind: str = "ladies"):
+        if kind not in ("ladies", "subgraph"):
+            raise ValueError("sampler configuration is wrong")  # main.py:88
+        self.sample_fn = smp.ladies_sample_host if kind == "ladies" else smp.subgraph_sample_host
         self.graph = smp.native_graph(lap)
         self.labels = labels_full
         self.train = np.asarray(train_nodes)
@@ -96,7 +99,7 @@ class BatchLoader:
         self.pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="gnn-sampler")
 
     def _produce(self, seed: int, nodes: np.ndarray) -> LoadedBatch:
-        hb = smp.ladies_sample_host(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels,
+        hb = self.sample_fn(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels,
                                     self.orders, self.dev_of, self.idx_on, None, 1.0, self.devices)
         hb.pin()
         plan = staging.make_plan(hb, self.store, self.rank, self.world, self.devices) if self.store else None

@@ -153,8 +153,9 @@ def native_graph(lap) -> NativeGraph:
     return g
 
 
-def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders):
-    """Run gnn_ladies_sample and copy the result out: (layers, sampled_nodes, input_nodes)."""
+def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies"):
+    """Run gnn_ladies_sample / gnn_subgraph_sample and copy the result out:
+    (layers, sampled_nodes, input_nodes, pinned tensors)."""
     import ctypes
 
     from . import _lib
@@ -166,9 +167,9 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders)
     od = np.ascontiguousarray(orders, dtype=np.int32)
     ptr = lambda a: None if a is None else a.ctypes.data
     h = ctypes.c_void_p()
-    _lib.check_sampler(L.gnn_ladies_sample(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), graph.num_nodes,
-                                           ptr(bn), bn.size, ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF,
-                                           ctypes.byref(h)), "gnn_ladies_sample")
+    fn = L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample
+    _lib.check_sampler(fn(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), graph.num_nodes, ptr(bn), bn.size,
+                          ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF, ctypes.byref(h)), f"gnn_{kind}_sample")
     # Outputs land straight in pinned host tensors (when a GPU is present): HostBatch.pin()
     # then has nothing left to copy and the H2D copies can be asynchronous.
     pin = torch.cuda.is_available()
@@ -290,6 +291,84 @@ def _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_ful
                      input_nodes_mask_on_devices=masks, input_nodes_mask_on_cpu=input_nodes_mask_on_cpu,
                      nodes_idx_on_devices=idxs, nodes_idx_on_cpu=nodes_idx_on_cpu, batch_nodes=batch_nodes,
                      labels=labels, seed=int(seed))
+
+
+def subgraph_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
+                         orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
+                         skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
+                         native: bool = True, device=None) -> HostBatch:
+    """subgraph_sampler (sampler.py:7-88) without the device work: one importance draw, then
+    the top-most non-zero-order layer takes lap[batch, :][:, after] and every layer below it
+    the square lap[after, :][:, after] (whatever its order, as the reference does), all with
+    the same normfact. native=False (and scale_factor > 1, where the reference scales the
+    counts of the columns placed on ``device``) runs the numpy restatement."""
+    batch_nodes = np.asarray(batch_nodes)
+    if native and not scale_factor > 1:
+        g = native_graph(lap_matrix)
+        if g.num_nodes != num_nodes:
+            raise ValueError("num_nodes does not match lap_matrix")
+        layers, sampled_nodes, after, pinned = _native_layers(seed, batch_nodes, samp_num_list, g, list(orders),
+                                                              kind="subgraph")
+        hb = _finish_batch(layers, sampled_nodes, after, batch_nodes, labels_full, device_id_of_nodes,
+                           idx_of_nodes_on_device, devices, seed)
+        lab = torch.from_numpy(hb.labels)
+        hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        return hb
+    if isinstance(lap_matrix, NativeGraph):
+        lap_matrix = lap_matrix.lap
+    np.random.seed(seed)
+    orders1 = list(orders)[::-1]
+    U = lap_matrix[batch_nodes, :]
+    U.sum_duplicates()
+    pi = column_nnz_counts(U, num_nodes)
+    if scale_factor > 1:
+        on_gpu = device_id_of_nodes == device
+        pi[on_gpu] = pi[on_gpu] * scale_factor
+    p = pi / np.sum(pi)
+    s_num = np.min([np.sum(p > 0), samp_num_list[0]])
+    after = np.random.choice(num_nodes, s_num, p=p, replace=False)
+    after = np.unique(np.concatenate((after, batch_nodes)))
+    normfact = 1 / np.clip(s_num * p[after], 1e-10, 1).astype(np.float32)
+
+    def layer(Ur):
+        adj = Ur[:, after]
+        return HostLayer(fullrowptr=Ur.indptr.astype(np.int32), rowptr=adj.indptr.astype(np.int32),
+                         colidx=adj.indices.astype(np.int32), normfact=normfact.copy(),
+                         shape=(int(adj.shape[0]), int(adj.shape[1])))
+
+    layers: List[Optional[HostLayer]] = []
+    sampled_nodes: List[np.ndarray] = []
+    layer_idx = 0
+    for d in range(len(orders1)):
+        layer_idx += 1
+        if orders1[d] == 0:
+            layers.append(None)
+            sampled_nodes.append(np.zeros(0, dtype=np.int64))
+        else:
+            layers.append(layer(U))
+            sampled_nodes.append(np.where(np.isin(after, batch_nodes))[0])
+            break
+    for d in range(layer_idx, len(orders1)):
+        Ua = lap_matrix[after, :]
+        Ua.sum_duplicates()
+        layers.append(layer(Ua))
+        sampled_nodes.append(np.arange(len(after)))
+    layers.reverse()
+    sampled_nodes.reverse()
+    return _finish_batch(layers, sampled_nodes, after, batch_nodes, labels_full, device_id_of_nodes,
+                         idx_of_nodes_on_device, devices, seed)
+
+
+def subgraph_sampler(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,
+                     device_id_of_nodes, idx_of_nodes_on_device, skewed_sampling_nodes, scale_factor, rank, devices):
+    """Reference signature and return tuple (sampler.py:7, :88)."""
+    dev = devices[rank]
+    hb = subgraph_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,
+                              device_id_of_nodes, idx_of_nodes_on_device, skewed_sampling_nodes, scale_factor,
+                              devices, device=dev)
+    db = hb.to_device(torch.device("cuda", dev) if isinstance(dev, int) else dev)
+    return (db.adjs, hb.input_nodes_mask_on_devices, hb.input_nodes_mask_on_cpu, hb.nodes_idx_on_devices,
+            hb.nodes_idx_on_cpu, hb.num_input_nodes, db.labels, hb.sampled_nodes)
 
 
 def ladies_sampler(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,

@@ -41,6 +41,15 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
 
+/* subgraph_sampler (sampler.py:7-88): ONE importance draw from the batch's neighbourhood
+ * (same p, s_num = min(#(p > 0), samp_num[0]), same RNG use), after = unique(sampled ∪ batch);
+ * the top-most layer with a non-zero order gets lap[batch, :][:, after]; every layer below it
+ * (whatever its order — reference behaviour) gets the square lap[after, :][:, after] with the
+ * same normfact and sampled_nodes = arange(len(after)). Same result object as LADIES. */
+int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                        const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                        const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
+
 /* dims of layer `layer` (bottom-up, as the returned adjs): {M, K, nnz, n_sampled, s_num}.
  * Returns 1 if the layer has order 0 (no sub-graph), 0 otherwise. */
 int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dims[5]);

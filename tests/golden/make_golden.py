@@ -15,7 +15,7 @@ What is pinned by executing the reference: LADIES sampling (RNG sequence, sub-gr
 normfact, sampled_nodes, placement masks), create_buffer placement maps, torch.sparse.mm
 SpMM outputs, and a GraphSAGE/GCN forward/backward/Adam step with the reference modules.
 
-Usage: python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage: python tests/golden/make_golden.py [--subgraph]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -228,5 +228,58 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+def subgraph_goldens():
+    """subgraph_sampler (sampler.py:7-88) outputs -> subgraph_tiny.npz (same tiny graph and
+    placement as graph_tiny.npz / placement_tiny.npz)."""
+    install_stubs()
+    import sampler as ref_sampler  # noqa: E402
+    import utils as ref_utils  # noqa: E402
+
+    A, labels, _, ncls, train, valid, test = make_dataset(TINY, seed=1, with_features=False)
+    N = A.shape[0]
+    lap = ref_utils.row_normalize(A).tocsr()
+    pl = np.load(os.path.join(HERE, "placement_tiny.npz"))
+    out = {}
+    rng = np.random.default_rng(17)
+    cases = [(512, 128, 31, 1, [1, 1, 1]), (64, 16, 5, 2, [1, 1, 1]), (256, 64, 8, 4, [0, 1, 1]),
+             (128, 32, 77, 1, [1, 0, 1])]
+    for ci, (samp, bs, seed, ndev, orders) in enumerate(cases):
+        batch = rng.choice(train, bs, replace=False)
+        devs = list(range(ndev))
+        RECORD.clear()
+        res = ref_sampler.subgraph_sampler(seed, batch, np.array([samp] * 5), N, lap, labels, orders,
+                                           pl[f"n{ndev}_dev0"], pl[f"n{ndev}_idx"], None, 1.0, 0, devs)
+        adjs, masks, cpu_mask, idx_dev, idx_cpu, nin, ylab, sampled = res
+        p = f"c{ci}_"
+        out[p + "cfg"] = np.array([samp, bs, seed, ndev])
+        out[p + "orders"] = np.array(orders)
+        out[p + "batch"] = batch.astype(np.int64)
+        out[p + "ncalls"] = len(RECORD)
+        for li, rec in enumerate(RECORD):  # top-down order of the create_coo_tensor calls
+            for key in ("fullrowptr", "rowptr", "colidx", "normfact"):
+                out[f"{p}call{li}_{key}"] = rec[key]
+            out[f"{p}call{li}_shape"] = np.array(rec["shape"])
+        for li, a in enumerate(adjs):
+            out[f"{p}present{li}"] = a is not None
+            out[f"{p}sampled{li}"] = np.asarray(sampled[li]).astype(np.int64)
+            if a is not None:
+                a = a.coalesce()
+                out[f"{p}adj{li}_indices"] = a.indices().numpy()
+                out[f"{p}adj{li}_values"] = a.values().numpy()
+        for i in range(ndev):
+            out[f"{p}mask{i}"] = np.asarray(masks[i])
+            out[f"{p}idxdev{i}"] = np.asarray(idx_dev[i]).astype(np.int64)
+        out[p + "cpumask"] = np.asarray(cpu_mask)
+        out[p + "idxcpu"] = np.asarray(idx_cpu).astype(np.int64)
+        out[p + "nin"] = nin
+        out[p + "labels"] = ylab.numpy()
+    np.savez_compressed(os.path.join(HERE, "subgraph_tiny.npz"), **out)
+    print("subgraph fixtures written to", HERE)
+
+
 if __name__ == "__main__":
-    main()
+    if "--subgraph" in sys.argv:
+        subgraph_goldens()
+    else:
+        main()
+        subgraph_goldens()

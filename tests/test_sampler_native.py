@@ -50,19 +50,29 @@ def _same(a, b):
     assert np.array_equal(a.labels, b.labels)
 
 
-def _both(lap, N, batch, samp, orders, seed, ndev=2):
+def _both(lap, N, batch, samp, orders, seed, ndev=2, kind="ladies"):
     dev_of = np.where(np.arange(N) % 3 == 0, -1, np.arange(N) % ndev)
     idx_on = np.arange(N) // 3
     args = (seed, batch, np.array(samp), N, lap, _labels(N), orders, dev_of, idx_on, None, 1.0, list(range(ndev)))
-    return (sampler.ladies_sample_host(*args, native=True), sampler.ladies_sample_host(*args, native=False))
+    fn = sampler.ladies_sample_host if kind == "ladies" else sampler.subgraph_sample_host
+    return fn(*args, native=True), fn(*args, native=False)
 
 
+@pytest.mark.parametrize("kind", ["ladies", "subgraph"])
 @pytest.mark.parametrize("samp,bs,seed", [(64, 16, 3), (512, 128, 11), (2048, 256, 99), (5000, 300, 7)])
-def test_native_matches_numpy(samp, bs, seed):
+def test_native_matches_numpy(samp, bs, seed, kind):
     N = 6000
     lap = _lap(N, 20, seed)
     batch = np.random.default_rng(seed).permutation(N)[:bs]
-    a, b = _both(lap, N, batch, [samp] * 3, [1, 1, 1], seed)
+    a, b = _both(lap, N, batch, [samp] * 3, [1, 1, 1], seed, kind=kind)
+    _same(a, b)
+
+
+@pytest.mark.parametrize("orders", [[0, 1, 1], [1, 0, 1], [0, 0, 1], [0, 0, 0]])
+def test_subgraph_orders(orders):
+    N = 2000
+    lap = _lap(N, 10, 8)
+    a, b = _both(lap, N, np.arange(100, 164), [300] * 3, orders, 21, kind="subgraph")
     _same(a, b)
 
 

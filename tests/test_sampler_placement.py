@@ -88,3 +88,56 @@ def test_rank_batches_partition():
         assert all(len(b) <= 64 for b in bs)
         seen.extend(np.concatenate(bs).tolist())
     assert sorted(seen) == nodes.tolist()
+
+
+def _rows_as_sets_equal(rowptr, a, b):
+    for r in range(len(rowptr) - 1):
+        s, e = rowptr[r], rowptr[r + 1]
+        if not np.array_equal(np.sort(a[s:e]), np.sort(b[s:e])):
+            return False
+    return True
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_subgraph_sampler_matches_reference(golden, native):
+    """subgraph_sampler (sampler.py:7-88) vs the reference's own outputs. Below the first
+    layer the reference slices the (unsorted) lap without canonicalising it, so its recorded
+    colidx rows are permutations of ours: rows compared as sets, and the operand the GPU
+    builds (the coalesced COO) compared exactly."""
+    _, lap, labels, _, N = _graph(golden)
+    z = golden("subgraph_tiny.npz")
+    pl = golden("placement_tiny.npz")
+    for c in range(4):
+        samp, bs, seed, ndev = (int(v) for v in z[f"c{c}_cfg"])
+        orders = [int(v) for v in z[f"c{c}_orders"]]
+        hb = sampler.subgraph_sample_host(seed, z[f"c{c}_batch"], np.array([samp] * 5), N, lap, labels, orders,
+                                          pl[f"n{ndev}_dev0"], pl[f"n{ndev}_idx"], None, 1.0, list(range(ndev)),
+                                          native=native)
+        nl = len(orders)
+        present = [li for li in range(nl) if bool(z[f"c{c}_present{li}"])]
+        assert [li for li in range(nl) if hb.layers[li] is not None] == present
+        assert int(z[f"c{c}_ncalls"]) == len(present)
+        for k, li in enumerate(sorted(present, reverse=True)):  # calls recorded top-down
+            L = hb.layers[li]
+            p = f"c{c}_call{k}_"
+            assert np.array_equal(L.fullrowptr, z[p + "fullrowptr"])
+            assert np.array_equal(L.rowptr, z[p + "rowptr"])
+            assert _rows_as_sets_equal(L.rowptr, L.colidx, z[p + "colidx"].astype(np.int32))
+            assert np.array_equal(L.normfact, z[p + "normfact"])
+            assert tuple(L.shape) == tuple(z[p + "shape"])
+            # the operand as the reference's create_coo_tensor + coalesce sees it
+            rows = np.repeat(np.arange(L.shape[0]), np.diff(L.rowptr))
+            deg = np.diff(L.fullrowptr).astype(np.float64)
+            vals = ((1.0 / deg[rows]) * L.normfact[L.colidx].astype(np.float64)).astype(np.float32)
+            order = np.lexsort((L.colidx, rows))
+            assert np.array_equal(np.stack([rows[order], L.colidx[order]]), z[f"c{c}_adj{li}_indices"])
+            assert np.array_equal(vals[order], z[f"c{c}_adj{li}_values"])
+        for li in range(nl):
+            assert np.array_equal(np.asarray(hb.sampled_nodes[li], np.int64), z[f"c{c}_sampled{li}"])
+        for i in range(ndev):
+            assert np.array_equal(hb.input_nodes_mask_on_devices[i], z[f"c{c}_mask{i}"])
+            assert np.array_equal(hb.nodes_idx_on_devices[i], z[f"c{c}_idxdev{i}"])
+        assert np.array_equal(hb.input_nodes_mask_on_cpu, z[f"c{c}_cpumask"])
+        assert np.array_equal(hb.nodes_idx_on_cpu, z[f"c{c}_idxcpu"])
+        assert hb.num_input_nodes == int(z[f"c{c}_nin"])
+        assert np.array_equal(hb.labels, z[f"c{c}_labels"])
