@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batches", type=int, default=4, help="distinct pre-sampled batches per rank (cycled)")
-    ap.add_argument("--model", default="graphsage")
+    ap.add_argument("--model", default="graphsage", choices=["graphsage", "gcn"])
+    ap.add_argument("--sampler", default="ladies", choices=["ladies", "subgraph", "fastgcn"])
     ap.add_argument("--samp-num", type=int, default=8192)
     ap.add_argument("--batch-size", type=int, default=512)
     ap.add_argument("--nhid", type=int, default=512)
@@ -70,8 +71,10 @@ def sample_batches(args, lap, labels, train, pl, rank, world):
     rs = np.random.RandomState(1234 + rank)
     seeds = rs.randint(2**31 - 1, size=len(batches))
     out = []
+    fn = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
+          "fastgcn": sampler.fastgcn_sample_host}[args.sampler]
     for s, b in zip(seeds, batches):
-        out.append(sampler.ladies_sample_host(int(s), b, np.array([args.samp_num] * 5), lap.shape[0], lap, labels,
+        out.append(fn(int(s), b, np.array([args.samp_num] * 5), lap.shape[0], lap, labels,
                                               [1, 1, 1], pl.device_id_of_nodes_group[rank],
                                               pl.idx_of_nodes_on_device_group[rank], None, 1.0, list(range(world))))
     return out
@@ -158,9 +161,29 @@ def cpu_baseline(args, hb, feats, num_classes):
         if time.perf_counter() - t0 >= args.cpu_baseline_seconds or n >= 50:
             break
     dt = time.perf_counter() - t0
+    # the aggregation calls alone: torch.sparse.mm forward, and backward
+    # including the reference's A.transpose(0,1).coalesce()
+    calls = {}
+    g = torch.Generator().manual_seed(0)
+    for li in (0, 1):
+        a = adjs[li]
+        X = x0 if li == 0 else torch.randn(a.shape[1], 2 * args.nhid, generator=g)
+        reps, t = 0, time.perf_counter()
+        while reps < 3 or (time.perf_counter() - t < 1.0 and reps < 20):
+            torch.sparse.mm(a, X)
+            reps += 1
+        calls[f"fwd{li}"] = round(1e3 * (time.perf_counter() - t) / reps, 2)
+        if li == 1:
+            G = torch.randn(a.shape[0], 2 * args.nhid, generator=g)
+            reps, t = 0, time.perf_counter()
+            while reps < 3 or (time.perf_counter() - t < 1.0 and reps < 20):
+                torch.sparse.mm(a.t().coalesce(), G)
+                reps += 1
+            calls["bwd1_incl_transpose"] = round(1e3 * (time.perf_counter() - t) / reps, 2)
     return {"value": n / dt, "unit": "mini-batches/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"{n} full GraphSAGE training steps (torch.sparse.mm fwd/bwd, dense layers, Adam) on "
-                      f"pre-sampled batch 0 (samp {args.samp_num}, bs {args.batch_size}), {dt:.1f} s"}
+                      f"pre-sampled batch 0 (samp {args.samp_num}, bs {args.batch_size}), {dt:.1f} s",
+            "spmm_call_ms": calls}
 
 
 def default_workers(world: int) -> int:
@@ -177,7 +200,7 @@ def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):
     workers = args.workers or default_workers(world)
     ld = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pl.device_id_of_nodes_group[rank],
                      pl.idx_of_nodes_on_device_group[rank], rank=rank, world_size=world, store=store,
-                     workers=workers, seed=4242)
+                     workers=workers, seed=4242, kind=args.sampler)
     it = ld.forever()
 
     def nxt():
@@ -297,6 +320,7 @@ def main():
 
     run(args.warmup, 0)
     cso.enable_timing(not args.no_roofline)
+    stager.timing = []
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -312,6 +336,11 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     recs = cso.take_timing_records()
+    h_bytes, h_sec = stager.take_timing()
+    staging_info = {"host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
+                    "h2d_GBps": round(h_bytes / h_sec / 1e9, 1) if h_sec > 0 else None,
+                    "h2d_ms_per_batch": round(1e3 * h_sec / args.steps, 3),
+                    "note": "pinned host rows -> HBM on the staging stream, overlapped with the previous step"}
 
     # ------------------------------------------------- end to end, live sampling
     e2e = None
@@ -389,7 +418,13 @@ def main():
             "dtype": "f32",
             "data": "synthetic (Chung-Lu Reddit-shaped graph, N(0,1) features, random-init GraphSAGE); "
                     f"{nb} pre-sampled LADIES batches per rank cycled, operands resident in HBM",
-            "config": {"workload": "Reddit GraphSAGE LADIES samp_num=8192 batch_size=512 (BASELINE config 2)",
+            "config": {"workload": (f"Reddit {'GraphSAGE' if args.model == 'graphsage' else 'GCN'} "
+                                    f"{args.sampler.upper() if args.sampler != 'fastgcn' else 'FastGCN'} "
+                                    f"samp_num={args.samp_num} batch_size={args.batch_size}"
+                                    + (" (BASELINE config 2)" if (args.model, args.sampler, args.samp_num,
+                                                                  args.batch_size) == ("graphsage", "ladies", 8192, 512)
+                                       and args.graph == "reddit" else "")),
+                       "sampler": args.sampler,
                        "model": args.model, "global_batch": args.batch_size * world, "samp_num": args.samp_num,
                        "nhid": args.nhid, "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
@@ -399,6 +434,7 @@ def main():
             "cpu_baseline": cpu,
             "spmm_per_callsite": spmm_detail,
             "end_to_end": e2e,
+            "feature_staging": staging_info,
             "final_loss": round(final_loss, 5),
         }
         print(json.dumps(line), flush=True)

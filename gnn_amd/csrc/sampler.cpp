@@ -92,9 +92,9 @@ struct Layer {
 // cumsum over the zero entries adds +0.0 (exact) and searchsorted('right') never lands on a
 // zero-probability index, so both run over the ascending list of currently non-zero
 // entries `live` with identical results.
-void choice_without_replacement(MT19937& rng, const std::vector<int32_t>& cnt, double total,
-                                std::vector<int64_t> live, int64_t size, std::vector<uint8_t>& taken,
-                                std::vector<int64_t>& found) {
+template <class Prob>
+void choice_without_replacement(MT19937& rng, Prob prob, std::vector<int64_t> live, int64_t size,
+                                std::vector<uint8_t>& taken, std::vector<int64_t>& found) {
   found.clear();
   found.reserve((size_t)size);
   std::vector<double> xs, cdf;
@@ -111,7 +111,7 @@ void choice_without_replacement(MT19937& rng, const std::vector<int32_t>& cnt, d
     cdf.resize(live.size());
     double s = 0.0;
     for (size_t i = 0; i < live.size(); ++i) {
-      s += (double)cnt[(size_t)live[i]] / total;
+      s += prob(live[i]);
       cdf[i] = s;
     }
     const double last = s;
@@ -176,6 +176,11 @@ class Work {
     return isum;
   }
 
+  // p[v] = pi[v] / sum(pi) for the column counts (sampler.py:122)
+  auto count_prob(double total) const {
+    return [this, total](int64_t v) { return (double)cnt[(size_t)v] / total; };
+  }
+
   void clear_counts() {
     for (int64_t c : live) cnt[(size_t)c] = 0;
   }
@@ -230,6 +235,17 @@ class Work {
     for (size_t j = 0; j < cols.size(); ++j) {
       double q = sn * ((double)cnt[(size_t)cols[j]] / total);
       q = q < 1e-10 ? 1e-10 : (q > 1.0 ? 1.0 : q);  // NaN passes through, as np.clip
+      L.normfact[j] = 1.0f / (float)q;
+    }
+  }
+
+  // same, with p given: 1 / float32(clip(s_num * p[cols], 1e-10, 1))
+  static void normfact_p(const std::vector<int64_t>& cols, const double* p, int64_t s_num, Layer& L) {
+    L.normfact.resize(cols.size());
+    const double sn = (double)s_num;
+    for (size_t j = 0; j < cols.size(); ++j) {
+      double q = sn * p[cols[j]];
+      q = q < 1e-10 ? 1e-10 : (q > 1.0 ? 1.0 : q);
       L.normfact[j] = 1.0f / (float)q;
     }
   }
@@ -308,7 +324,7 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
       const double total = (double)isum;
       const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[d]);
       L.s_num = s_num;
-      choice_without_replacement(rng, w.cnt, total, w.live, s_num, w.taken, w.found);
+      choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
       w.make_after(prev, after);
       w.extract(prev, unnz, L);
       w.normfact(after, total, s_num, L);
@@ -349,7 +365,7 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
     if (isum == 0) return fail("gnn_subgraph_sample: probabilities contain NaN (no entries in U)");
     const double total = (double)isum;
     const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[0]);
-    choice_without_replacement(rng, w.cnt, total, w.live, s_num, w.taken, w.found);
+    choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
     w.make_after(batch, after);
     // ... the top-most layer with a non-zero order takes U[:, after] (sampler.py:42-53) ...
     int32_t d = 0;
@@ -386,6 +402,54 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_subgraph_sample: out of host memory");
+  }
+}
+
+int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                       const double* p, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
+  if (int rc = check_inputs("gnn_fastgcn_sample", indptr, indices, num_nodes, batch_nodes, batch_size, samp_num,
+                            orders, num_layers, out))
+    return rc;
+  if (!p) return fail("gnn_fastgcn_sample: p is NULL");
+  *out = nullptr;
+  try {
+    const Graph g{indptr, indices, data, (size_t)num_nodes};
+    Work w(g);
+    std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
+    res->layers.resize((size_t)num_layers);
+    MT19937 rng(seed);
+    // the layer-independent importance: live = ascending nodes with p > 0 (NaN p never live)
+    std::vector<int64_t> live;
+    for (int64_t v = 0; v < num_nodes; ++v)
+      if (p[v] > 0.0) live.push_back(v);
+    std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size), after;
+    for (int32_t d = 0; d < num_layers; ++d) {
+      Layer& L = res->layers[(size_t)(num_layers - 1 - d)];
+      if (orders[num_layers - 1 - d] == 0) continue;
+      L.present = true;
+      const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
+      if (unnz < 0) return fail("gnn_fastgcn_sample: sub-graph nnz >= 2^31");
+      const int64_t s_num = std::min<int64_t>((int64_t)live.size(), samp_num[d]);
+      L.s_num = s_num;
+      choice_without_replacement(rng, [p](int64_t v) { return p[v]; }, live, s_num, w.taken, w.found);
+      // after = unique(sampled): layers are sampled independently (no union with prev)
+      after.assign(w.found.begin(), w.found.end());
+      std::sort(after.begin(), after.end());
+      for (int64_t v : w.found) w.taken[(size_t)v] = 0;
+      w.set_columns(after);
+      w.extract(prev, unnz, L);
+      Work::normfact_p(after, p, s_num, L);
+      w.positions(after, prev, L);
+      L.M = (int64_t)prev.size();
+      L.K = (int64_t)after.size();
+      prev.swap(after);
+    }
+    res->input_nodes = prev;
+    *out = res.release();
+    return 0;
+  } catch (const std::bad_alloc&) {
+    return fail("gnn_fastgcn_sample: out of host memory");
   }
 }
 

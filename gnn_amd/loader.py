@@ -78,9 +78,11 @@ class BatchLoader:
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
                  seed: int = 0, devices=None, kind: str = "ladies"):
-        if kind not in ("ladies", "subgraph"):
+        fns = {"ladies": smp.ladies_sample_host, "subgraph": smp.subgraph_sample_host,
+               "fastgcn": smp.fastgcn_sample_host}
+        if kind not in fns:
             raise ValueError("sampler configuration is wrong")  # main.py:88
-        self.sample_fn = smp.ladies_sample_host if kind == "ladies" else smp.subgraph_sample_host
+        self.sample_fn = fns[kind]
         self.graph = smp.native_graph(lap)
         self.labels = labels_full
         self.train = np.asarray(train_nodes)
@@ -99,8 +101,8 @@ class BatchLoader:
         self.pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="gnn-sampler")
 
     def _produce(self, seed: int, nodes: np.ndarray) -> LoadedBatch:
-        hb = self.sample_fn(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels,
-                                    self.orders, self.dev_of, self.idx_on, None, 1.0, self.devices)
+        hb = self.sample_fn(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels, self.orders,
+                            self.dev_of, self.idx_on, None, 1.0, self.devices)
         hb.pin()
         plan = staging.make_plan(hb, self.store, self.rank, self.world, self.devices) if self.store else None
         return LoadedBatch(hb, plan)

@@ -137,6 +137,13 @@ class NativeGraph:
         # data == 0 entries are structure but not counted (ord-0 norm); skip the array if none
         self.data = None if np.all(data != 0) else np.ascontiguousarray(data, dtype=np.float32)
         self.lap = lap
+        self._fastgcn_p = None
+
+    @property
+    def fastgcn_p(self) -> np.ndarray:
+        if self._fastgcn_p is None:
+            self._fastgcn_p = fastgcn_probability(self.lap)
+        return self._fastgcn_p
 
 
 _native_graphs: "dict[int, NativeGraph]" = {}
@@ -167,9 +174,13 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
     od = np.ascontiguousarray(orders, dtype=np.int32)
     ptr = lambda a: None if a is None else a.ctypes.data
     h = ctypes.c_void_p()
-    fn = L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample
-    _lib.check_sampler(fn(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), graph.num_nodes, ptr(bn), bn.size,
-                          ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF, ctypes.byref(h)), f"gnn_{kind}_sample")
+    g3 = (ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), graph.num_nodes)
+    rest = (ptr(bn), bn.size, ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF, ctypes.byref(h))
+    if kind == "fastgcn":
+        rc = L.gnn_fastgcn_sample(*g3, ptr(graph.fastgcn_p), *rest)
+    else:
+        rc = (L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample)(*g3, *rest)
+    _lib.check_sampler(rc, f"gnn_{kind}_sample")
     # Outputs land straight in pinned host tensors (when a GPU is present): HostBatch.pin()
     # then has nothing left to copy and the H2D copies can be asynchronous.
     pin = torch.cuda.is_available()
@@ -357,6 +368,75 @@ def subgraph_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix
     sampled_nodes.reverse()
     return _finish_batch(layers, sampled_nodes, after, batch_nodes, labels_full, device_id_of_nodes,
                          idx_of_nodes_on_device, devices, seed)
+
+
+def fastgcn_probability(lap) -> np.ndarray:
+    """FastGCN's layer-independent importance q(u) ∝ ||lap[:, u]||² (Chen et al. 2018; the
+    form LADIES' reference code uses: column sums of lap∘lap), float64, normalised."""
+    lap = sp.csr_matrix(lap)
+    d = np.asarray(lap.data, dtype=np.float64)
+    pi = np.bincount(lap.indices, weights=d * d, minlength=lap.shape[1])
+    return pi / np.sum(pi)
+
+
+def fastgcn_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
+                        orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
+                        skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
+                        native: bool = True) -> HostBatch:
+    """FastGCN sampler (BASELINE config 5; NOT in the reference, so parity is unpinned — the
+    native and numpy versions below are checked against each other and for their sampling
+    law). Per layer, top-down: s_num = min(#(p > 0), samp_num[d]) nodes drawn with the global
+    importance p (np.random.choice without replacement, same RNG stream as LADIES), the
+    sub-graph U[:, after] with the reference operator's normfact convention. Layers are
+    independent (no union with the previous nodes), so it suits GCN, not GraphSAGE's
+    x[sampled_nodes] self features."""
+    batch_nodes = np.asarray(batch_nodes)
+    g = native_graph(lap_matrix)
+    if native:
+        layers, sampled_nodes, inp, pinned = _native_layers(seed, batch_nodes, samp_num_list, g, list(orders),
+                                                            kind="fastgcn")
+        hb = _finish_batch(layers, sampled_nodes, inp, batch_nodes, labels_full, device_id_of_nodes,
+                           idx_of_nodes_on_device, devices, seed)
+        lab = torch.from_numpy(hb.labels)
+        hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        return hb
+    lap = g.lap
+    p = g.fastgcn_p
+    np.random.seed(seed)
+    previous = batch_nodes
+    layers: List[Optional[HostLayer]] = []
+    sampled_nodes: List[np.ndarray] = []
+    orders1 = list(orders)[::-1]
+    for d in range(len(orders1)):
+        if orders1[d] == 0:
+            layers.append(None)
+            sampled_nodes.append(np.zeros(0, dtype=np.int64))
+            continue
+        U = lap[previous, :]
+        s_num = np.min([np.sum(p > 0), samp_num_list[d]])
+        after = np.unique(np.random.choice(num_nodes, s_num, p=p, replace=False))
+        adj = U[:, after]
+        layers.append(HostLayer(fullrowptr=U.indptr.astype(np.int32), rowptr=adj.indptr.astype(np.int32),
+                                colidx=adj.indices.astype(np.int32),
+                                normfact=1 / np.clip(s_num * p[after], 1e-10, 1).astype(np.float32),
+                                shape=(int(adj.shape[0]), int(adj.shape[1]))))
+        sampled_nodes.append(np.where(np.isin(after, previous))[0])
+        previous = after
+    layers.reverse()
+    sampled_nodes.reverse()
+    return _finish_batch(layers, sampled_nodes, previous, batch_nodes, labels_full, device_id_of_nodes,
+                         idx_of_nodes_on_device, devices, seed)
+
+
+def fastgcn_sampler(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,
+                    device_id_of_nodes, idx_of_nodes_on_device, skewed_sampling_nodes, scale_factor, rank, devices):
+    """Same signature and return tuple as the reference's samplers (sampler.py:7, :90)."""
+    dev = devices[rank]
+    hb = fastgcn_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,
+                             device_id_of_nodes, idx_of_nodes_on_device, skewed_sampling_nodes, scale_factor, devices)
+    db = hb.to_device(torch.device("cuda", dev) if isinstance(dev, int) else dev)
+    return (db.adjs, hb.input_nodes_mask_on_devices, hb.input_nodes_mask_on_cpu, hb.nodes_idx_on_devices,
+            hb.nodes_idx_on_cpu, hb.num_input_nodes, db.labels, hb.sampled_nodes)
 
 
 def subgraph_sampler(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full, orders,

@@ -108,6 +108,15 @@ class Stager:
         self.device = store.device
         self.stream = torch.cuda.Stream(device=self.device)
         self.exchange = exchange
+        self.timing: Optional[list] = None  # set to [] to record (event, event, bytes) per host copy
+
+    def take_timing(self):
+        """(host bytes, seconds) summed over the recorded host-row copies; clears the record."""
+        recs, self.timing = self.timing or [], None
+        if not recs:
+            return 0, 0.0
+        recs[-1][1].synchronize()
+        return sum(b for _, _, b in recs), sum(a.elapsed_time(b) for a, b, _ in recs) * 1e-3
 
     def issue(self, plan: StagePlan):
         dev = self.device
@@ -116,7 +125,13 @@ class Stager:
         with torch.cuda.stream(st):
             x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
             own_pos, own_src, host_pos = (t.to(dev, non_blocking=True) for t in plan.pinned)
+            if self.timing is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
             host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
+            if self.timing is not None:
+                e1.record(st)
+                self.timing.append((e0, e1, plan.host_rows.numel() * 4))
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
             if len(plan.host_pos):
                 cso.gather_rows(host_dev, None, x0, host_pos, n=len(plan.host_pos))

@@ -50,6 +50,17 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
                         const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                         const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
 
+/* FastGCN layer-wise sampler (Chen et al. 2018; NOT in the reference — BASELINE config 5;
+ * parity unpinned): p is the caller's layer-independent importance over all nodes
+ * (fastgcn_probability: column sums of lap∘lap, normalised); per layer, top-down,
+ * U = lap[prev, :], s_num = min(#(p > 0), samp_num[d]), np.random.choice(N, s_num, p=p,
+ * replace=False) on the same RNG stream as LADIES, after = unique(sampled) (no union with
+ * prev), adj = U[:, after], normfact = 1 / float32(clip(s_num * p[after], 1e-10, 1)).
+ * Same result object as LADIES. */
+int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                       const double* p, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
+
 /* dims of layer `layer` (bottom-up, as the returned adjs): {M, K, nnz, n_sampled, s_num}.
  * Returns 1 if the layer has order 0 (no sub-graph), 0 otherwise. */
 int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dims[5]);

@@ -54,11 +54,12 @@ def _both(lap, N, batch, samp, orders, seed, ndev=2, kind="ladies"):
     dev_of = np.where(np.arange(N) % 3 == 0, -1, np.arange(N) % ndev)
     idx_on = np.arange(N) // 3
     args = (seed, batch, np.array(samp), N, lap, _labels(N), orders, dev_of, idx_on, None, 1.0, list(range(ndev)))
-    fn = sampler.ladies_sample_host if kind == "ladies" else sampler.subgraph_sample_host
+    fn = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
+          "fastgcn": sampler.fastgcn_sample_host}[kind]
     return fn(*args, native=True), fn(*args, native=False)
 
 
-@pytest.mark.parametrize("kind", ["ladies", "subgraph"])
+@pytest.mark.parametrize("kind", ["ladies", "subgraph", "fastgcn"])
 @pytest.mark.parametrize("samp,bs,seed", [(64, 16, 3), (512, 128, 11), (2048, 256, 99), (5000, 300, 7)])
 def test_native_matches_numpy(samp, bs, seed, kind):
     N = 6000
@@ -139,6 +140,33 @@ def test_native_isolated_batch_raises_like_numpy():
         with pytest.raises((ValueError, RuntimeError), match="NaN"):
             sampler.ladies_sample_host(0, np.arange(4), np.array([8] * 3), N, lap, _labels(N), [1, 1, 1],
                                        np.full(N, -1), np.zeros(N, np.int64), None, 1.0, [0], native=native)
+
+
+def test_fastgcn_sampling_law():
+    """FastGCN (parity unpinned: not in the reference): drawn nodes follow the global
+    importance p ∝ column sums of lap∘lap — chi-square-style check of inclusion frequencies
+    on the top-probability nodes, and the operand convention (normfact from p)."""
+    N = 3000
+    lap = _lap(N, 12, 13)
+    p = sampler.fastgcn_probability(lap)
+    assert abs(p.sum() - 1) < 1e-12
+    dense = lap.toarray().astype(np.float64)
+    np.testing.assert_allclose(p, (dense ** 2).sum(0) / (dense ** 2).sum(), rtol=1e-12)
+    s = 40
+    hits = np.zeros(N)
+    trials = 400
+    dev_of = np.full(N, -1)
+    for t in range(trials):
+        hb = sampler.fastgcn_sample_host(t, np.arange(10), np.array([s] * 3), N, lap, _labels(N), [1],
+                                         dev_of, np.zeros(N, np.int64), None, 1.0, [0])
+        hits[hb.input_nodes] += 1
+        L = hb.layers[0]
+        q = np.clip(s * p[hb.input_nodes], 1e-10, 1).astype(np.float32)
+        assert np.array_equal(L.normfact, 1 / q)
+    # without replacement, inclusion prob ~ s*p for small p: compare on the mid-probability nodes
+    mid = np.argsort(p)[-200:-20]
+    expect = trials * s * p[mid]
+    assert abs(hits[mid].sum() / expect.sum() - 1) < 0.1
 
 
 def test_native_errors():
