@@ -225,19 +225,20 @@ def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):
         el = float(t.item())
     out = {"value": round(world * args.e2e_steps / el, 3), "unit": "mini-batches/s", "steps": args.e2e_steps,
            "sampler_workers_per_rank": workers,
-           "what": "live LADIES sampling (native, worker threads) + pinned host staging + H2D + the same step"}
+           "what": f"live {args.sampler} sampling (native, worker threads) + pinned host staging + H2D + the same step"}
     if rank == 0:
         chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
+        fn = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
+              "fastgcn": sampler.fastgcn_sample_host}[args.sampler]
         sm = np.array([args.samp_num] * 5)
         pdev, pidx = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
         t = time.perf_counter()
         for i, c in enumerate(chunks[:3]):
-            sampler.ladies_sample_host(i, c, sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0,
-                                       list(range(world)))
+            fn(i, c, sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)))
         nat = (time.perf_counter() - t) / 3
         t = time.perf_counter()
-        sampler.ladies_sample_host(3, chunks[3], sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0,
-                                   list(range(world)), native=False)
+        fn(3, chunks[3], sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)),
+           native=False)
         npy = time.perf_counter() - t
         out["sampler_ms_per_batch_1thread"] = {"native": round(nat * 1e3, 1), "numpy": round(npy * 1e3, 1)}
     return out
