@@ -92,12 +92,28 @@ def _counter_rows(d):
     return rows
 
 
-def pmc_traffic(hb, F, workdir="/tmp/gnn_bench_pmc"):
-    """HBM-side bytes per launch of the layer-0 forward aggregation kernel from rocprofv3 PMC
-    counters (FETCH_SIZE and WRITE_SIZE in separate passes), corrected by calibrating each
-    counter on a row gather of known bytes with the same row and vector width
-    (MI355X_MICROARCH.md §HBM). Runs the probe as a CHILD process before this process has
-    touched the GPU. Returns a dict, or None if the profiler is unavailable."""
+def _kernel_symbol(name: str) -> str:
+    """'void (anonymous namespace)::spmm_unit_kernel<4, 16, 1, 4, false>(int const*, ...)' ->
+    'spmm_unit_kernel<4, 16, 1, 4, false>' (the form the bench's timing records use)."""
+    name = name.split("(anonymous namespace)::")[-1]
+    depth = 0
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return name[:i].strip()
+    return name.strip()
+
+
+def pmc_traffic(hb, F, hidden, workdir="/tmp/gnn_bench_pmc"):
+    """Bytes per launch leaving L2 (toward the Infinity Cache / HBM) for each aggregation
+    kernel instantiation, from rocprofv3 PMC counters (FETCH_SIZE and WRITE_SIZE in separate
+    passes) over the forward calls of batch 0 laid out as the benchmark runs them, each
+    counter corrected by a calibration gather of known bytes with the same 16-byte row
+    vectors (MI355X_MICROARCH.md §HBM). Runs the probe as a CHILD process before this process
+    has touched the GPU. Returns {"by_kernel": {symbol: {...}}, corrections}, or None."""
     import shutil
     import subprocess
 
@@ -110,39 +126,42 @@ def pmc_traffic(hb, F, workdir="/tmp/gnn_bench_pmc"):
                      for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
              **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
     probe = os.path.join(REPO, "scripts", "pmc_probe.py")
-    vals = {}
+    calib, kern = {}, {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(workdir, counter)
         shutil.rmtree(d, ignore_errors=True)
         cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
-               sys.executable, probe, npz, "--feat", str(F)]
+               sys.executable, probe, npz, "--feat", str(F), "--hidden", str(hidden)]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             log(f"pmc pass {counter} failed rc={r.returncode}: {r.stderr[-500:]}")
             return None
-        calib, spmm = [], []
+        cal = []
         for row in _counter_rows(d):
             if row.get("Counter_Name") != counter:
                 continue
             name, v = row.get("Kernel_Name", ""), float(row.get("Counter_Value", "nan"))
             if "gather_rows_kernel" in name:
-                calib.append(v)
+                cal.append(v)
             elif "spmm_unit_kernel" in name:
-                spmm.append(v)
-        if not calib or not spmm:
+                kern.setdefault(_kernel_symbol(name), {}).setdefault(counter, []).append(v)
+        if not cal:
             return None
-        vals[counter] = (float(np.median(calib)), float(np.median(spmm)))
-    n = int(1.2e9 // (F * 4))
-    known = n * F * 4  # bytes read (and written) by one calibration gather
-    fc, fs = vals["FETCH_SIZE"]
-    wc, ws = vals["WRITE_SIZE"]
-    read_corr = known / (fc * 1024.0)
-    write_corr = known / (wc * 1024.0)
-    read_b = fs * 1024.0 * read_corr
-    write_b = ws * 1024.0 * write_corr
-    return {"bytes_per_launch": read_b + write_b, "read_bytes": read_b, "write_bytes": write_b,
-            "fetch_size_kb_raw": fs, "write_size_kb_raw": ws, "read_correction": round(read_corr, 4),
-            "write_correction": round(write_corr, 4)}
+        calib[counter] = float(np.median(cal))
+    ld = (F + 3) // 4 * 4
+    n = int(1.2e9 // (ld * 4))
+    known = n * ld * 4  # bytes read (and written) by one calibration gather
+    read_corr = known / (calib["FETCH_SIZE"] * 1024.0)
+    write_corr = known / (calib["WRITE_SIZE"] * 1024.0)
+    by = {}
+    for sym, c in kern.items():
+        if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
+            continue
+        rd = float(np.mean(c["FETCH_SIZE"])) * 1024.0 * read_corr
+        wr = float(np.mean(c["WRITE_SIZE"])) * 1024.0 * write_corr
+        by[sym] = {"bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                   "launches": len(c["FETCH_SIZE"])}
+    return {"by_kernel": by, "read_correction": round(read_corr, 4), "write_correction": round(write_corr, 4)}
 
 
 def cpu_baseline(args, hb, feats, num_classes):
@@ -266,7 +285,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_traffic:
         # before this process initialises the GPU: the probe is a child process
         try:
-            traffic = pmc_traffic(host_batches[0], feats.shape[1])
+            traffic = pmc_traffic(host_batches[0], feats.shape[1], 2 * args.nhid)
         except Exception as e:  # profiler trouble must not sink the benchmark
             log(f"pmc traffic measurement skipped: {e!r}")
         log(f"pmc traffic done ({time.time() - t0:.1f}s): {traffic}")
@@ -370,30 +389,45 @@ def main():
     roof = None
     spmm_detail = {}
     if recs:
-        # per call site: tag "fwd"/"bwd" + call order within the step (3 fwd, 2 bwd)
-        per_step = 5
-        site = {}
-        for i, (tag, ms, nbytes) in enumerate(recs):
-            key = f"{tag}{i % per_step}"
+        # per call site, in call order within a step: 3 forwards, then the backwards of
+        # layers 2 and 1 (layer 0's input needs no gradient)
+        names = ["fwd_L0", "fwd_L1", "fwd_L2", "bwd_L2", "bwd_L1"]
+        site, kname = {}, {}
+        for i, (tag, ms, nbytes, kn) in enumerate(recs):
+            key = names[i % len(names)]
+            assert key.startswith(tag), (key, tag)
             e = site.setdefault(key, [0.0, 0, 0])
             e[0] += ms
             e[1] += nbytes
             e[2] += 1
+            kname[key] = kn
         for key, (ms, nbytes, n) in site.items():
             spmm_detail[key] = {"avg_us": 1e3 * ms / n, "GB_per_launch": nbytes / n / 1e9,
-                                "GBps": nbytes / (ms * 1e-3) / 1e9}
-        dom = max(site, key=lambda k_: site[k_][0])
-        ms, nbytes, n = site[dom]
+                                "GBps": nbytes / (ms * 1e-3) / 1e9, "kernel": kname[key]}
+        # the dominant kernel = the aggregation instantiation (as rocprofv3 names it) with the
+        # most time per step; several call sites may share it (rocprof averages over them too)
+        byk = {}
+        for key, (ms_, nb_, n_) in site.items():
+            e = byk.setdefault(kname[key], [0.0, 0, 0, []])
+            e[0] += ms_
+            e[1] += nb_
+            e[2] += n_
+            e[3].append(key)
+        dom = max(byk, key=lambda k_: byk[k_][0])
+        ms, nbytes, n, sites = byk[dom]
         achieved = nbytes / (ms * 1e-3) / 1e9
+        tr = (traffic or {}).get("by_kernel", {}).get(dom)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 # GB per launch leaving L2 for the Infinity Cache / HBM (PMC, calibrated)
-                "traffic": round(traffic["bytes_per_launch"] / 1e9, 4) if traffic else None,
-                "kernel": f"spmm_unit_kernel ({'layer-0 forward' if dom == 'fwd0' else dom}), "
-                          f"avg {1e3 * ms / n:.1f} us/launch over {n} launches, "
-                          f"{nbytes / n / 1e9:.3f} GB algorithmic per launch"}
-        if traffic:
-            roof["traffic_detail"] = traffic
+                "traffic": round(tr["bytes_per_launch"] / 1e9, 4) if tr else None,
+                "kernel": f"{dom} (call sites {' + '.join(sorted(sites))}), avg {1e3 * ms / n:.1f} us/launch over "
+                          f"{n} launches, {nbytes / n / 1e9:.3f} GB algorithmic per launch"}
+        if tr:
+            roof["traffic_detail"] = dict(tr, read_correction=traffic["read_correction"],
+                                          write_correction=traffic["write_correction"],
+                                          all_kernels={k: round(v["bytes_per_launch"] / 1e9, 4)
+                                                       for k, v in traffic["by_kernel"].items()})
         tot_ms = sum(v[0] for v in site.values())
         tot_b = sum(v[1] for v in site.values())
         roof["all_spmm_GBps"] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)

@@ -124,7 +124,7 @@ __device__ __forceinline__ int wave_first_true(int lo, int hi, int lane, Pred pr
 // Slab layout: [nunits][2][ldslab]; slot 0 = piece of a row that began in an earlier unit,
 // slot 1 = piece of a row that begins in this unit and continues past it.
 // ---------------------------------------------------------------------------------
-template <int VW, int G, int NJ, int U>
+template <int VW, int G, int NJ, int U, bool RES>
 __global__ __launch_bounds__(256) void spmm_unit_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
     int M, int nnz, int S, int nunits,
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
     const float* res = nullptr;  // residual row added to a complete output row
     if (rb >= ustart && re <= uend) {
       dst = Y + (int64_t)r * ldy;
-      if (rmap) {
+      if constexpr (RES) {
         const int q = rmap[r];
         if (q >= 0) res = R + (int64_t)q * ldr;
       }
@@ -231,7 +231,9 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
       const int cc = c0 + j * G * VW;
       if ((j % P) == sub && cc < F) {
         V a = acc[j];
-        if (res) a += *reinterpret_cast<const V*>(res + cc);
+        if constexpr (RES) {
+          if (res) a += *reinterpret_cast<const V*>(res + cc);
+        }
         *reinterpret_cast<V*>(dst + cc) = a;
       }
     }
@@ -910,41 +912,43 @@ using MainFn = void (*)(const int*, const int*, const float*, int, int, int, int
 constexpr int pick_u(int nj) { return nj <= 4 ? 4 : (nj == 5 ? 3 : 2); }
 
 template <int VW, int G, int NJ>
-MainFn main_ptr() {
-  return &spmm_unit_kernel<VW, G, NJ, pick_u(NJ)>;
+MainFn main_ptr(bool res) {
+  return res ? &spmm_unit_kernel<VW, G, NJ, pick_u(NJ), true> : &spmm_unit_kernel<VW, G, NJ, pick_u(NJ), false>;
 }
 
 template <int VW, int G>
-MainFn main_by_nj(int nj) {
+MainFn main_by_nj(int nj, bool res) {
   switch (nj) {
-    case 1: return main_ptr<VW, G, 1>();
-    case 2: return main_ptr<VW, G, 2>();
-    case 3: return main_ptr<VW, G, 3>();
-    case 4: return main_ptr<VW, G, 4>();
-    case 5: return main_ptr<VW, G, 5>();
-    case 6: return main_ptr<VW, G, 6>();
-    case 7: return main_ptr<VW, G, 7>();
-    case 8: return main_ptr<VW, G, 8>();
+    case 1: return main_ptr<VW, G, 1>(res);
+    case 2: return main_ptr<VW, G, 2>(res);
+    case 3: return main_ptr<VW, G, 3>(res);
+    case 4: return main_ptr<VW, G, 4>(res);
+    case 5: return main_ptr<VW, G, 5>(res);
+    case 6: return main_ptr<VW, G, 6>(res);
+    case 7: return main_ptr<VW, G, 7>(res);
+    case 8: return main_ptr<VW, G, 8>(res);
     default: return nullptr;
   }
 }
 
 template <int VW>
-MainFn main_by_g(int g, int nj) {
+MainFn main_by_g(int g, int nj, bool res) {
   switch (g) {
-    case 64: return main_by_nj<VW, 64>(nj);
-    case 32: return main_by_nj<VW, 32>(nj);
-    case 16: return main_by_nj<VW, 16>(nj);
-    case 8: return main_by_nj<VW, 8>(nj);
+    case 64: return main_by_nj<VW, 64>(nj, res);
+    case 32: return main_by_nj<VW, 32>(nj, res);
+    case 16: return main_by_nj<VW, 16>(nj, res);
+    case 8: return main_by_nj<VW, 8>(nj, res);
     default: return nullptr;
   }
 }
 
-MainFn select_main(const SpmmCfg& c) {
+// res: the row-mapped residual variant (gnn_spmm_csr_f32_ex); a separate instantiation, so
+// the plain aggregation carries no residual code and the two show up apart in rocprofv3.
+MainFn select_main(const SpmmCfg& c, bool res) {
   switch (c.vw) {
-    case 4: return main_by_g<4>(c.g, c.nj);
-    case 2: return main_by_g<2>(c.g, c.nj);
-    case 1: return main_by_g<1>(c.g, c.nj);
+    case 4: return main_by_g<4>(c.g, c.nj, res);
+    case 2: return main_by_g<2>(c.g, c.nj, res);
+    case 1: return main_by_g<1>(c.g, c.nj, res);
     default: return nullptr;
   }
 }
@@ -1059,7 +1063,7 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
   GNN_REQUIRE((uintptr_t)workspace % 16 == 0, "gnn_spmm_csr_f32: workspace not 16-byte aligned");
   GNN_REQUIRE(rmap == nullptr || (ldr % c.vw == 0 && (uintptr_t)R % (4 * c.vw) == 0),
               "gnn_spmm_csr_f32_ex: R (ldr %lld) not aligned for %d-wide vectors", (long long)ldr, c.vw);
-  MainFn fn = select_main(c);
+  MainFn fn = select_main(c, rmap != nullptr);
   GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no kernel for vw=%d g=%d nj=%d", c.vw, c.g, c.nj);
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;

@@ -44,16 +44,17 @@ def enable_timing(flag: bool = True) -> None:
 
 
 def take_timing_records(sync: bool = True):
-    """Return [(tag, ms, algorithmic_bytes)] for recorded calls and clear the list.
+    """Return [(tag, ms, algorithmic_bytes, kernel_name)] for recorded calls and clear the list
+    (kernel_name as rocprofv3 lists the main kernel: spmm_unit_kernel<VW, G, NJ, U>).
 
     Also folds the times into spmm_forward_time / spmm_backward_time (seconds)."""
     global spmm_forward_time, spmm_backward_time
     if sync and _timing_records:
         _timing_records[-1][2].synchronize()
     out = []
-    for tag, e0, e1, nbytes in _timing_records:
+    for tag, e0, e1, nbytes, kname in _timing_records:
         ms = e0.elapsed_time(e1)
-        out.append((tag, ms, nbytes))
+        out.append((tag, ms, nbytes, kname))
         if tag.startswith("fwd"):
             spmm_forward_time += ms * 1e-3
         else:
@@ -210,7 +211,15 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
             e0.record()  # creates the underlying hipEvent; the library re-records it
             e1.record()
             L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
-            _timing_records.append((tag, e0, e1, algorithmic_bytes(M, op.nnz, F)))
+            cfg = (ctypes.c_int32 * 6)()
+            L.gnn_spmm_config(M, K, op.nnz, Fk, ldx, Fk, dense.data_ptr(), out.data_ptr(), unit_nnz, cfg)
+            u = 4 if cfg[2] <= 4 else (3 if cfg[2] == 5 else 2)  # pick_u (spmm.hip)
+            nbytes = algorithmic_bytes(M, op.nnz, F)
+            if rmap is not None:  # residual rows read + the row map
+                nbytes += residual.shape[0] * F * 4 + M * 4
+            res = "true" if rmap is not None else "false"
+            _timing_records.append((tag, e0, e1, nbytes,
+                                    f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>"))
         if rmap is None:
             _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
                                           dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,

@@ -9,7 +9,7 @@ timeout -k 10 600 python bench.py --dump-batch /tmp/gnnprof/batch0.npz > gpurun_
 timeout -k 10 300 python scripts/spmm_microbench.py /tmp/gnnprof/batch0.npz --units ${UNITS:-0,4,8,16,64,256} \
     --out gpurun_out/micro_$TAG.json > gpurun_out/micro_$TAG.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/gnnprof/prof -o run -- \
-    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err
+    python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-traffic --no-e2e > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err
 rc=$?
 find /tmp/gnnprof/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats_$TAG.csv \;
 echo "exit $rc"

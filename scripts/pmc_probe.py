@@ -5,7 +5,9 @@
    every row of a 1.2 GB table (> the 256 MiB Infinity Cache) exactly once, in random order,
    with the SAME row width / vector width as the aggregation kernel being measured, so the
    read bytes are known exactly.
-2. The layer-0 forward aggregation of the benchmark's batch 0 (the dominant kernel), R times.
+2. The forward aggregations of the benchmark's batch 0, R times each, with the operands laid
+   out as bench.py runs them (layer 0: X0 in 604-float padded rows; layers 1-2: 1024 wide),
+   so the kernel instantiations — the names rocprofv3 reports — are the benchmark's.
 """
 import argparse
 import os
@@ -22,32 +24,39 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("batch")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--layer", type=int, default=0)
+    ap.add_argument("--hidden", type=int, default=1024, help="width of the layer-1/2 inputs ((1+order)*nhid)")
     ap.add_argument("--feat", type=int, default=602)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     F = args.feat
-    # calibration table: rows of F floats, contiguous (same vector width as the SpMM)
-    n = int(1.2e9 // (F * 4))
+    ld = (F + 3) // 4 * 4
+    # calibration table: rows of ld floats (16-byte vectors, as the aggregation's X0 reads)
+    n = int(1.2e9 // (ld * 4))
     g = torch.Generator(device=dev).manual_seed(0)
-    table = torch.empty((n, F), dtype=torch.float32, device=dev).normal_(generator=g)
+    table = torch.empty((n, ld), dtype=torch.float32, device=dev).normal_(generator=g)
     perm = torch.randperm(n, device=dev, generator=g)
-    out = torch.empty((n, F), dtype=torch.float32, device=dev)
+    out = torch.empty((n, ld), dtype=torch.float32, device=dev)
     for _ in range(2):
         cso.gather_rows(table, perm, out, None, n=n)
     torch.cuda.synchronize()
     del table, out, perm
     z = np.load(args.batch)
-    li = args.layer
-    shape = tuple(int(v) for v in z[f"l{li}_shape"])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    op, _ = cso.build_operand(t(z[f"l{li}_fullrowptr"]), t(z[f"l{li}_rowptr"]), t(z[f"l{li}_colidx"]),
-                              t(z[f"l{li}_normfact"]), shape[0], shape[1], with_coo=False)
-    X = torch.randn(shape[1], F, device=dev)
-    for _ in range(args.reps):
-        cso.spmm_csr(op, X)
-    torch.cuda.synchronize()
-    print(f"calib_rows={n} row_bytes={F * 4} M={shape[0]} K={shape[1]} nnz={op.nnz} F={F}", flush=True)
+    for li in range(3):
+        shape = tuple(int(v) for v in z[f"l{li}_shape"])
+        op, _ = cso.build_operand(t(z[f"l{li}_fullrowptr"]), t(z[f"l{li}_rowptr"]), t(z[f"l{li}_colidx"]),
+                                  t(z[f"l{li}_normfact"]), shape[0], shape[1], with_coo=False)
+        if li == 0:
+            X = torch.zeros((shape[1], ld), device=dev)
+            X[:, :F].normal_()
+            X = X[:, :F]
+        else:
+            X = torch.randn(shape[1], args.hidden, device=dev)
+        for _ in range(args.reps):
+            cso.spmm_csr(op, X)
+        torch.cuda.synchronize()
+        print(f"layer {li}: M={shape[0]} K={shape[1]} nnz={op.nnz} F={X.shape[1]} ldx={X.stride(0)}", flush=True)
+    print(f"calib_rows={n} row_bytes={ld * 4}", flush=True)
 
 
 if __name__ == "__main__":

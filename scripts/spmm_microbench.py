@@ -32,7 +32,7 @@ def time_call(op, X, unit, reps):
     cso.enable_timing(False)
     ms = np.array([r[1] for r in recs])
     tms =np.array([a.elapsed_time(b) for a, b in tot])
-    return float(np.median(ms)), recs[0][2], float(np.median(tms))
+    return float(np.median(ms)), recs[0][2], float(np.median(tms))  # (tag, ms, bytes, kernel)
 
 
 def main():
