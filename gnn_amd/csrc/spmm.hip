@@ -12,10 +12,10 @@
 //  * Load balance without a scan: the nonzeros are cut into fixed work units of S
 //    consecutive entries (S = unit_nnz). One 64-lane wave owns one unit; it finds its
 //    first/last row with a 64-way parallel search of rowptr and walks the rows in order.
-//    A row wholly inside a unit is stored straight to Y (empty rows store zeros, so Y is
-//    never memset); a row cut by a unit boundary stores its two partial sums to a slab,
-//    and a small second kernel adds the pieces in unit order. No atomics: results are
-//    deterministic.
+//    A row of at most S nonzeros is owned whole by the unit holding its first nonzero and
+//    stored straight to Y (empty rows store zeros, so Y is never memset); only longer rows
+//    are cut at unit boundaries: their pieces go to a slab and a small second kernel adds
+//    them in unit order. No atomics: results are deterministic.
 //  * Inside a wave, G lanes span the feature columns with VW-wide (8 or 16 byte) loads,
 //    NJ column chunks per lane, and the 64/G lane groups take different nonzeros of the
 //    same row; U nonzeros are issued back to back so U*NJ row loads are in flight per lane
@@ -28,6 +28,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 #include <string>
 
 #include "gnn_spmm.h"
@@ -145,6 +147,9 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
   const int uend = min(ustart + S, nnz);
   const bool last = (u == nunits - 1);
 
+  // Row ownership: a row of at most S nonzeros belongs wholly to the unit holding its first
+  // nonzero (it may run past uend, by < S); only longer rows are cut at unit boundaries.
+  // rlo = the row containing position ustart (or the first row starting at/after it).
   const int rlo = wave_first_true(0, M, lane, [&](int r) {
     return rowptr[r + 1] > ustart || rowptr[r] >= ustart;
   });
@@ -153,8 +158,10 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
   for (int r = rlo; r < rhi; ++r) {
     const int rb = rowptr[r];
     const int re = rowptr[r + 1];
+    const bool cut = re - rb > S;  // wave-uniform
+    if (rb < ustart && !cut) continue;  // short row owned by an earlier unit
     const int b = max(rb, ustart);
-    const int e = min(re, uend);
+    const int e = cut ? min(re, uend) : re;
     V acc[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[j] = vzero<VW>();
@@ -217,7 +224,7 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
 
     float* dst;
     const float* res = nullptr;  // residual row added to a complete output row
-    if (rb >= ustart && re <= uend) {
+    if (!cut) {
       dst = Y + (int64_t)r * ldy;
       if constexpr (RES) {
         const int q = rmap[r];
@@ -240,9 +247,12 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
   }
 }
 
-// Adds the unit pieces of every row that straddles a unit boundary, in unit order.
-// Grid-stride over rows (a capped grid: most rows are not split and exit at once); a wave
-// sums one split row, its lanes spanning the columns.
+// Adds the unit pieces of every cut row (> S nonzeros), in unit order. A workgroup covers
+// 16 rows: every wave loads their rowptr pairs at once (one dependent round, not one per
+// row) and ballots the cut ones; the (cut row, 64*VW-column pass) items are dealt to the 4
+// waves, so a cluster of long rows still spreads over the workgroup.
+constexpr int COMBINE_ROWS = 16;
+
 template <int VW>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int* __restrict__ rowptr, int M, int S,
@@ -251,15 +261,26 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
   using V = typename Vec<VW>::T;
   const int lane = threadIdx.x & 63;
-  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < M; r += gridDim.x * 4) {
+  const int w = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * COMBINE_ROWS;
+  const int rl = r0 + lane;
+  const bool is_cut = lane < COMBINE_ROWS && rl < M && (rowptr[rl + 1] - rowptr[rl]) > S;  // ownership rule
+  const unsigned long long cutmask = __ballot(is_cut);
+  if (cutmask == 0ull) return;
+  const int npass = (F + 64 * VW - 1) / (64 * VW);
+  const int items = __builtin_popcountll(cutmask) * npass;
+  for (int it = w; it < items; it += 4) {
+    unsigned long long m = cutmask;
+    for (int k = it / npass; k > 0; --k) m &= m - 1;  // the (it / npass)-th cut row
+    const int r = r0 + __builtin_ctzll(m);
+    const int cc = (it % npass) * 64 * VW + lane * VW;
+    if (cc >= F) continue;
     const int rb = rowptr[r];
     const int re = rowptr[r + 1];
-    if (re == rb) continue;
     const int u0 = rb / S;
     const int u1 = (re - 1) / S;
-    if (u0 == u1) continue;
     const int q = rmap ? rmap[r] : -1;
-    for (int cc = lane * VW; cc < F; cc += 64 * VW) {
+    {
       V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
       int u = u0 + 1;
       for (; u + 4 <= u1 + 1; u += 4) {
@@ -281,7 +302,9 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
 
 // ---------------------------------------------------------------------------------
 // Operand builder: value = (float)((1.0 / full_degree(row)) * (double)normfact[col]),
-// the formula of cuda_spmm.cu:800 evaluated in double. One wave per row.
+// the formula of cuda_spmm.cu:800 evaluated in double. A flat nnz-balanced pass builds
+// every entry; rows found out of column order (never from a scipy-sliced sub-graph, but a
+// caller may pass them) are redone by a row-per-wave pass that also sorts them.
 // ---------------------------------------------------------------------------------
 // Bitonic sort helpers, "all comparators ascending" form: positions >= L act as +inf.
 constexpr int SEG_WAVE_LDS = 512;
@@ -310,21 +333,14 @@ __device__ __forceinline__ void bitonic_pair(int p, int size, int d, bool flip, 
   }
 }
 
-// Also restores the coalesced (column-ascending) order the reference gets from
-// .coalesce(): rows found unsorted are sorted here when short (<= 64 entries, in
-// registers) or queued for the segmented sorters (counters[0]: <= SEG_BLOCK_LDS entries,
-// counters[1]: longer). Sorted rows — scipy's slicing output — cost nothing extra.
+// One row by one wave: values, a sortedness check and, for an unsorted row, the sort that
+// restores the coalesced (column-ascending) order the reference gets from .coalesce():
+// in registers (<= 64 entries), in the wave's LDS (<= 512) or in place in global memory.
 template <typename CT>
-__global__ __launch_bounds__(256) void build_operand_kernel(
-    const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
-    const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
-    int* __restrict__ out_col, float* __restrict__ out_val) {
-  __shared__ int sk[4][SEG_WAVE_LDS];
-  __shared__ float sv[4][SEG_WAVE_LDS];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int r = blockIdx.x * 4 + w;
-  if (r >= nrows) return;
+__device__ void build_operand_row(const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
+                                  const CT* __restrict__ colidx, const float* __restrict__ normfact, int r,
+                                  int* __restrict__ out_col, float* __restrict__ out_val, int* sk, float* sv,
+                                  int lane) {
   const int b = rowptr[r];
   const int e = rowptr[r + 1];
   if (b == e) return;
@@ -364,8 +380,8 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
   if (L <= SEG_WAVE_LDS) {
     for (int i = lane; i < n; i += 64) {
       const int c = (i < L) ? (int)colidx[b + i] : INT_MAX;
-      sk[w][i] = c;
-      sv[w][i] = (i < L) ? (float)(inv * (double)normfact[c]) : 0.0f;
+      sk[i] = c;
+      sv[i] = (i < L) ? (float)(inv * (double)normfact[c]) : 0.0f;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -377,13 +393,13 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
         int i, j;
         bitonic_pair(p, size, d, flip, i, j);
         if (L <= SEG_WAVE_LDS) {
-          const int ki = sk[w][i], kj = sk[w][j];
+          const int ki = sk[i], kj = sk[j];
           if (kj < ki) {
-            const float vi = sv[w][i], vj = sv[w][j];
-            sk[w][i] = kj;
-            sk[w][j] = ki;
-            sv[w][i] = vj;
-            sv[w][j] = vi;
+            const float vi = sv[i], vj = sv[j];
+            sk[i] = kj;
+            sk[j] = ki;
+            sv[i] = vj;
+            sv[j] = vi;
           }
         } else if (j < L) {
           const int ki = out_col[b + i], kj = out_col[b + j];
@@ -402,10 +418,63 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
   }
   if (L <= SEG_WAVE_LDS) {
     for (int i = lane; i < L; i += 64) {
-      out_col[b + i] = sk[w][i];
-      out_val[b + i] = sv[w][i];
+      out_col[b + i] = sk[i];
+      out_val[b + i] = sv[i];
     }
   }
+}
+
+// Row-per-wave build with the sort fallback; grid-stride over rows. With `flag`, a no-op
+// unless the flat builder of the same call (generation `gen`) saw an unsorted row.
+template <typename CT>
+__global__ __launch_bounds__(256) void build_operand_kernel(
+    const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
+    const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
+    int* __restrict__ out_col, float* __restrict__ out_val,
+    const unsigned long long* __restrict__ flag, unsigned long long gen) {
+  __shared__ int sk[4][SEG_WAVE_LDS];
+  __shared__ float sv[4][SEG_WAVE_LDS];
+  if (flag && *flag < gen) return;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  for (int r = blockIdx.x * 4 + w; r < nrows; r += gridDim.x * 4)
+    build_operand_row<CT>(fullrowptr, rowptr, colidx, normfact, r, out_col, out_val, sk[w], sv[w], lane);
+}
+
+// Flat build: a wave per 256 consecutive nonzeros (nnz-balanced, ~4 loads in flight per
+// lane), each lane finding its row by a short binary search between the chunk's first and
+// last rows. Writes col/val for every entry and raises `flag` to `gen` if any row is out of
+// order (then the row-per-wave kernel above re-does those rows with their sort).
+template <typename CT>
+__global__ __launch_bounds__(256) void build_operand_flat_kernel(
+    const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
+    const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows, int nnz,
+    int* __restrict__ out_col, float* __restrict__ out_val,
+    unsigned long long* __restrict__ flag, unsigned long long gen) {
+  const int lane = threadIdx.x & 63;
+  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 256;
+  if (cs >= nnz) return;
+  const int ce = min(cs + 256, nnz);
+  const int rf = wave_first_true(0, nrows, lane, [&](int r) { return rowptr[r + 1] > cs; });
+  const int rl = wave_first_true(rf, nrows, lane, [&](int r) { return rowptr[r + 1] >= ce; });
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int i = cs + t * 64 + lane;
+    if (i < ce) {
+      int lo = rf, hi = rl;  // the largest r with rowptr[r] <= i is the row holding i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (rowptr[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      const int c = (int)colidx[i];
+      if (i + 1 < rowptr[lo + 1]) bad |= c > (int)colidx[i + 1];
+      const double inv = 1.0 / (double)(fullrowptr[lo + 1] - fullrowptr[lo]);
+      out_col[i] = c;
+      out_val[i] = (float)(inv * (double)normfact[c]);
+    }
+  }
+  if (__ballot(bad) != 0ull && lane == 0) atomicMax(flag, gen);
 }
 
 // COO index image of a CSR: indices[0][i] = row(i), indices[1][i] = col[i].
@@ -996,6 +1065,32 @@ int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hi
   return 0;
 }
 
+// Per-device "unsorted row seen" word for the operand builder. Each build call takes a new
+// generation number; the flat pass raises the word to it (atomicMax) when it meets an
+// unsorted row and the fix pass runs only if the word is >= its generation. Concurrent
+// calls on other streams can only make a fix pass run needlessly, never skip a needed one.
+std::mutex g_flag_mu;
+unsigned long long* g_flag[64] = {};
+std::atomic<unsigned long long> g_gen{0};
+
+int operand_flag(unsigned long long** flag, unsigned long long* gen) {
+  int dev = 0;
+  GNN_HIP(hipGetDevice(&dev), "hipGetDevice");
+  GNN_REQUIRE(dev >= 0 && dev < 64, "operand builder: device id %d out of range", dev);
+  {
+    std::lock_guard<std::mutex> lk(g_flag_mu);
+    if (!g_flag[dev]) {
+      void* p = nullptr;
+      GNN_HIP(hipMalloc(&p, 256), "hipMalloc (operand flag)");
+      GNN_HIP(hipMemset(p, 0, 256), "hipMemset (operand flag)");
+      g_flag[dev] = (unsigned long long*)p;
+    }
+    *flag = g_flag[dev];
+  }
+  *gen = ++g_gen;
+  return 0;
+}
+
 }  // namespace
 
 // =================================================================================
@@ -1074,7 +1169,7 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
   GNN_LAUNCHED("spmm_unit_kernel");
   if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
-    const dim3 g2((unsigned)std::min<int64_t>(ceil_div(M, 4), 512));
+    const dim3 g2((unsigned)ceil_div(M, (int64_t)COMBINE_ROWS));
     switch (c.vw) {
       case 4:
         spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
@@ -1108,20 +1203,34 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
   GNN_REQUIRE(fullrowptr && rowptr && colidx && normfact && csr_col && csr_val, "gnn_build_operand_f32: NULL input");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)ceil_div(nrows, 4));
-  (void)workspace;  // rows are sorted in the build kernel itself; kept for ABI stability
+  (void)workspace;  // not needed (the unsorted-row flag lives in the library); ABI stability
   (void)workspace_bytes;
+  unsigned long long* flag = nullptr;
+  unsigned long long gen = 0;
+  if (int rc = operand_flag(&flag, &gen)) return rc;
+  const dim3 gflat((unsigned)ceil_div(nnz, 1024));  // 4 waves x 256 nonzeros
+  const dim3 gfix(256);
   switch (colidx_bytes) {
     case 2:
-      build_operand_kernel<int16_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+      build_operand_flat_kernel<int16_t><<<gflat, dim3(256), 0, st>>>(
+          fullrowptr, rowptr, (const int16_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
+      GNN_LAUNCHED("build_operand_flat_kernel");
+      build_operand_kernel<int16_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val, flag, gen);
       break;
     case 4:
-      build_operand_kernel<int32_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+      build_operand_flat_kernel<int32_t><<<gflat, dim3(256), 0, st>>>(
+          fullrowptr, rowptr, (const int32_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
+      GNN_LAUNCHED("build_operand_flat_kernel");
+      build_operand_kernel<int32_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val, flag, gen);
       break;
     default:
-      build_operand_kernel<int64_t><<<grid, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
-                                                                (int)nrows, csr_col, csr_val);
+      build_operand_flat_kernel<int64_t><<<gflat, dim3(256), 0, st>>>(
+          fullrowptr, rowptr, (const int64_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
+      GNN_LAUNCHED("build_operand_flat_kernel");
+      build_operand_kernel<int64_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
+                                                                (int)nrows, csr_col, csr_val, flag, gen);
       break;
   }
   GNN_LAUNCHED("build_operand_kernel");

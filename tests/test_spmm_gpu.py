@@ -210,6 +210,26 @@ def test_build_operand_long_rows(dev):
     assert np.array_equal(op.val.cpu().numpy(), oval)
 
 
+def test_build_operand_sorted_unsorted_sequence(dev):
+    """The flat builder's unsorted-row flag is per call (generation numbers): an unsorted
+    operand, then a sorted one, then unsorted again, on the same stream and on a second one."""
+    rng = np.random.default_rng(21)
+    M, K = 300, 2000
+    lens = powerlaw_lens(M, 50, 1.2, rng, K)
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    shuffled = col.copy()
+    for r in range(0, M, 3):
+        rng.shuffle(shuffled[rowptr[r]:rowptr[r + 1]])
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    side = torch.cuda.Stream(device=dev)
+    for c, st in ((shuffled, None), (col, None), (shuffled, side), (col, side), (shuffled, None)):
+        with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(dev)):
+            op = _op(dev, full, rowptr, c, nf, M, K)
+        torch.cuda.synchronize()
+        assert np.array_equal(op.col.cpu().numpy(), ocol)
+        assert np.array_equal(op.val.cpu().numpy(), oval)
+
+
 def test_transpose_bitexact(dev):
     M, K = 3000, 2000
     rng = np.random.default_rng(9)
