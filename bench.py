@@ -61,6 +61,7 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=60, help="steps of the live-sampling end-to-end run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the live-sampling end-to-end run")
     ap.add_argument("--workers", type=int, default=0, help="sampler threads per rank (0: auto)")
+    ap.add_argument("--cprofile", default="", help="after the timed run, cProfile 20 steps into this text file")
     ap.add_argument("--torch-profile", default="", help="after the timed run, write a torch.profiler op table here")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     return ap.parse_args()
@@ -346,6 +347,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     loss = run(args.steps, args.warmup)
+    t_issued = time.perf_counter()  # host done issuing (GPU-bound runs return early)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -366,6 +368,19 @@ def main():
     e2e = None
     if not args.no_e2e and args.e2e_steps > 0:
         e2e = end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev)
+    if args.cprofile and rank == 0:
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        run(20, 0)
+        torch.cuda.synchronize()
+        pr.disable()
+        with open(args.cprofile, "w") as fh:
+            st = pstats.Stats(pr, stream=fh)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumulative").print_stats(45)
     if args.torch_profile and rank == 0:
         from torch.profiler import ProfilerActivity, profile
 
@@ -447,6 +462,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "host_issue_ms_per_step": round(1e3 * (t_issued - t_start) / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

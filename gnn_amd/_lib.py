@@ -35,6 +35,7 @@ _SIGNATURES = {
     "gnn_spmm_set_timing_events": (None, [_VP, _VP]),
     "gnn_segsort_workspace_bytes": (_SZ, [_I64]),
     "gnn_build_operand_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "gnn_build_operand_t_f32": (_INT, [_VP, _VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP]),
     "gnn_coo_to_csr": (_INT, [_VP, _VP, _I64, _I64, _VP, _VP, _VP]),
     "gnn_csr_transpose_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "gnn_csr_transpose": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
@@ -46,6 +47,8 @@ _SIGNATURES = {
     "gnn_sage_norm_bwd_f32": (_INT, [_VP, _I64, _VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _VP, _I64,
                                      ctypes.c_float, ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ,
                                      _VP]),
+    "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
+    "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
 }
 
 EXPORTED_SYMBOLS = tuple(_SIGNATURES)
@@ -62,6 +65,7 @@ _SAMPLER_SIGNATURES = {
                                   ctypes.POINTER(_VP)]),
     "gnn_ladies_layer_dims": (_INT, [_VP, ctypes.c_int32, ctypes.POINTER(_I64)]),
     "gnn_ladies_layer_copy": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP]),
+    "gnn_ladies_layer_csc": (_INT, [_VP, ctypes.c_int32, _VP, _VP]),
     "gnn_ladies_num_input_nodes": (_I64, [_VP]),
     "gnn_ladies_input_nodes": (_INT, [_VP, _VP]),
     "gnn_ladies_free": (None, [_VP]),

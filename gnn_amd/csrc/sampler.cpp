@@ -479,6 +479,21 @@ int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fu
   return 0;
 }
 
+int gnn_ladies_layer_csc(const gnn_ladies_result* r, int32_t layer, int32_t* colptr, int32_t* rows) {
+  if (!r || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_csc: bad args");
+  const Layer& L = r->layers[(size_t)layer];
+  if (!L.present) return fail("gnn_ladies_layer_csc: layer %d has no sub-graph", layer);
+  if (!colptr || (!rows && !L.colidx.empty())) return fail("gnn_ladies_layer_csc: NULL output");
+  // stable counting sort of the entries by column: rows come out ascending in each column
+  std::fill(colptr, colptr + L.K + 1, 0);
+  for (int32_t c : L.colidx) ++colptr[c + 1];
+  for (int64_t c = 0; c < L.K; ++c) colptr[c + 1] += colptr[c];
+  std::vector<int32_t> cur(colptr, colptr + L.K);
+  for (int64_t i = 0; i < L.M; ++i)
+    for (int32_t k = L.rowptr[(size_t)i]; k < L.rowptr[(size_t)i + 1]; ++k) rows[cur[(size_t)L.colidx[(size_t)k]]++] = (int32_t)i;
+  return 0;
+}
+
 int64_t gnn_ladies_num_input_nodes(const gnn_ladies_result* r) { return r ? (int64_t)r->input_nodes.size() : -1; }
 
 int gnn_ladies_input_nodes(const gnn_ladies_result* r, int64_t* out) {

@@ -477,6 +477,35 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
   if (__ballot(bad) != 0ull && lane == 0) atomicMax(flag, gen);
 }
 
+// Values of the transposed operand from its CSR structure (the CSC of A): entry i of
+// transposed row c (a column of A) is A's entry (rows[i], c), value
+// (float)((1.0 / full_degree(rows[i])) * (double)normfact[c]) — bit-identical to the
+// forward operand's value of that entry, so (colptr, rows, val) IS the canonical transpose.
+__global__ __launch_bounds__(256) void build_operand_t_kernel(
+    const int* __restrict__ fullrowptr, const int* __restrict__ colptr, const int* __restrict__ rows,
+    const float* __restrict__ normfact, int ncols, int nnz, float* __restrict__ out_val) {
+  const int lane = threadIdx.x & 63;
+  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 256;
+  if (cs >= nnz) return;
+  const int ce = min(cs + 256, nnz);
+  const int cf = wave_first_true(0, ncols, lane, [&](int c) { return colptr[c + 1] > cs; });
+  const int cl = wave_first_true(cf, ncols, lane, [&](int c) { return colptr[c + 1] >= ce; });
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int i = cs + t * 64 + lane;
+    if (i < ce) {
+      int lo = cf, hi = cl;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (colptr[mid] <= i) lo = mid; else hi = mid - 1;
+      }
+      const int r = rows[i];
+      const double inv = 1.0 / (double)(fullrowptr[r + 1] - fullrowptr[r]);
+      out_val[i] = (float)(inv * (double)normfact[lo]);
+    }
+  }
+}
+
 // COO index image of a CSR: indices[0][i] = row(i), indices[1][i] = col[i].
 __global__ __launch_bounds__(256) void csr_to_coo_indices_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, int nrows, int64_t nnz,
@@ -1209,7 +1238,7 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
   unsigned long long gen = 0;
   if (int rc = operand_flag(&flag, &gen)) return rc;
   const dim3 gflat((unsigned)ceil_div(nnz, 1024));  // 4 waves x 256 nonzeros
-  const dim3 gfix(256);
+  const dim3 gfix(16);  // usually a no-op (gated): keep the launch small
   switch (colidx_bytes) {
     case 2:
       build_operand_flat_kernel<int16_t><<<gflat, dim3(256), 0, st>>>(
@@ -1238,6 +1267,19 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
     csr_to_coo_indices_kernel<<<grid, dim3(256), 0, st>>>(rowptr, csr_col, (int)nrows, nnz, coo_indices);
     GNN_LAUNCHED("csr_to_coo_indices_kernel");
   }
+  return 0;
+}
+
+int gnn_build_operand_t_f32(const int32_t* fullrowptr, const int32_t* colptr, const int32_t* rows,
+                            const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, float* val_t,
+                            void* stream) {
+  GNN_REQUIRE(nrows >= 0 && ncols >= 0 && nnz >= 0, "gnn_build_operand_t_f32: negative size");
+  GNN_REQUIRE(nrows < INT_MAX && ncols < INT_MAX && nnz < INT_MAX, "gnn_build_operand_t_f32: sizes must be < 2^31");
+  if (ncols == 0 || nnz == 0) return 0;
+  GNN_REQUIRE(fullrowptr && colptr && rows && normfact && val_t, "gnn_build_operand_t_f32: NULL input");
+  build_operand_t_kernel<<<dim3((unsigned)ceil_div(nnz, 1024)), dim3(256), 0, (hipStream_t)stream>>>(
+      fullrowptr, colptr, rows, normfact, (int)ncols, (int)nnz, val_t);
+  GNN_LAUNCHED("build_operand_t_kernel");
   return 0;
 }
 

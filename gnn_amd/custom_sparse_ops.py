@@ -294,6 +294,27 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
     return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
 
 
+def attach_transpose(op: CsrOperand, fullrowptr: torch.Tensor, colptr: torch.Tensor, rows: torch.Tensor,
+                     normfact: torch.Tensor) -> CsrOperand:
+    """Cache on ``op`` its transpose built from a caller-provided CSC structure (colptr,
+    rows: rows ascending per column, e.g. from the native sampler) — only the values are
+    computed on the GPU (gnn_build_operand_t_f32); the result equals op.transpose()."""
+    M, K = op.shape
+    _require(colptr.numel() == K + 1 and rows.numel() == op.nnz, "CSC structure does not match the operand")
+    for name, t in (("colptr", colptr), ("rows", rows)):
+        _require(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), f"{name} must be contiguous int32 CUDA")
+    dev = op.device
+    with torch.cuda.device(dev):
+        val = torch.empty(op.nnz, dtype=torch.float32, device=dev)
+        _lib.check(_lib.lib().gnn_build_operand_t_f32(_ptr(fullrowptr), _ptr(colptr), _ptr(rows), _ptr(normfact),
+                                                      M, K, op.nnz, _ptr(val), _stream(dev)),
+                   "gnn_build_operand_t_f32")
+    t = CsrOperand(colptr, rows, val, (K, M))
+    t._t = op
+    op._t = t
+    return t
+
+
 def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> torch.Tensor:
     """spmm.cpp:44-50 / cuda_spmm.cu:806-827: coalesced sparse COO of the sampled layer with
     value = (1/full_degree(row)) * normfact[col] (double math, fp32 store). The CSR image

@@ -49,7 +49,7 @@ class GraphSageConvolution(nn.Module):
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
     def forward_fused(self, x, adj, sampled_nodes, p, training):
-        from .fused import index_rows, linear_nobias, sage_aggregate, sage_norm
+        from .fused import index_rows, linear_pair, sage_aggregate, sage_norm
 
         bB, bW = self.linearB.bias, self.linearW.bias
         if self.order > 0:
@@ -57,10 +57,10 @@ class GraphSageConvolution(nn.Module):
                 feat, xs = sage_aggregate(adj, x, sampled_nodes)
             else:
                 feat, xs = self.spmm_fn(adj, x), index_rows(x, sampled_nodes)
-            hB = linear_nobias(xs, self.linearB.weight)
-            hW = linear_nobias(feat, self.linearW.weight)
+            hB, hW = linear_pair([xs, feat], [self.linearB.weight, self.linearW.weight])
             return sage_norm(hB, hW, self.scale, self.offset, p, training, bB, bW)
-        return sage_norm(None, linear_nobias(x, self.linearW.weight), self.scale, self.offset, p, training, None, bW)
+        (hW,) = linear_pair([x], [self.linearW.weight])
+        return sage_norm(None, hW, self.scale, self.offset, p, training, None, bW)
 
 
 class GraphSage(nn.Module):
@@ -109,11 +109,11 @@ class GraphConvolution(nn.Module):
         return (out - mean) * self.scale * torch.rsqrt(var) + self.offset
 
     def forward_fused(self, x, adj, p, training):
-        from .fused import linear_nobias, sage_norm
+        from .fused import linear_pair, sage_norm
 
         feat = self.spmm_fn(adj, x) if self.order > 0 else x
-        return sage_norm(None, linear_nobias(feat, self.linear.weight), self.scale, self.offset, p, training, None,
-                         self.linear.bias)
+        (h,) = linear_pair([feat], [self.linear.weight])
+        return sage_norm(None, h, self.scale, self.offset, p, training, None, self.linear.bias)
 
 
 class GCN(nn.Module):

@@ -31,6 +31,8 @@ class HostLayer:
     colidx: np.ndarray      # int32 [nnz]
     normfact: np.ndarray    # float32 [K]: 1 / float32(clip(s_num * p[after], 1e-10, 1))
     shape: tuple            # (M, K)
+    csc_colptr: Optional[np.ndarray] = None  # int32 [K+1]: CSC of the sub-graph (= CSR of its
+    csc_rows: Optional[np.ndarray] = None    # transpose, rows ascending per column), if made
 
 
 @dataclass
@@ -61,7 +63,10 @@ class HostBatch:
             pin = torch.cuda.is_available()
             t = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))
             p = lambda x: x.pin_memory() if pin else x
-            layers = [None if L is None else (p(t(L.fullrowptr)), p(t(L.rowptr)), p(t(L.colidx)), p(t(L.normfact)))
+            layers = [None if L is None else
+                      (p(t(L.fullrowptr)), p(t(L.rowptr)), p(t(L.colidx)), p(t(L.normfact)),
+                       None if L.csc_colptr is None else p(t(L.csc_colptr)),
+                       None if L.csc_rows is None else p(t(L.csc_rows)))
                       for L in self.layers]
             sampled = [p(t(s, np.int64)) for s in self.sampled_nodes]
             self.extra["pinned"] = (layers, sampled, p(t(self.labels)))
@@ -72,8 +77,8 @@ class HostBatch:
         build=False, run the operand builder. Returns a DeviceBatch."""
         dev = torch.device(device)
         layers, sampled, labels = self.pin().extra["pinned"]
-        d = lambda x: x.to(dev, non_blocking=True)
-        raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape)
+        d = lambda x: None if x is None else x.to(dev, non_blocking=True)
+        raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape, d(P[4]), d(P[5]))
                for P, L in zip(layers, self.layers)]
         db = DeviceBatch(self, raw, None, [d(s) for s in sampled], d(labels))
         if build:
@@ -84,7 +89,8 @@ class HostBatch:
 @dataclass
 class DeviceBatch:
     host: HostBatch
-    raw: list            # per layer: device (fullrowptr, rowptr, colidx, normfact, shape) or None
+    raw: list            # per layer: device (fullrowptr, rowptr, colidx, normfact, shape, csc_colptr|None,
+                         # csc_rows|None) or None
     adjs: Optional[list]
     sampled_nodes: list
     labels: torch.Tensor
@@ -98,8 +104,10 @@ class DeviceBatch:
             if r is None:
                 adjs.append(None)
                 continue
-            fr, rp, ci, nf, shape = r
+            fr, rp, ci, nf, shape, cp, cr = r
             op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo)
+            if cp is not None:  # host-made CSC: the backward's operand without a GPU transpose
+                cso.attach_transpose(op, fr, cp, cr, nf)
             if with_coo:
                 a = torch.sparse_coo_tensor(coo, op.val, shape, is_coalesced=True)
                 a._gnn_csr = op
@@ -160,9 +168,11 @@ def native_graph(lap) -> NativeGraph:
     return g
 
 
-def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies"):
-    """Run gnn_ladies_sample / gnn_subgraph_sample and copy the result out:
-    (layers, sampled_nodes, input_nodes, pinned tensors)."""
+def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies",
+                   csc_from: int = 1):
+    """Run gnn_ladies_sample / gnn_subgraph_sample / gnn_fastgcn_sample and copy the result
+    out: (layers, sampled_nodes, input_nodes, pinned tensors). Layers >= csc_from (those
+    whose input needs a gradient; layer 0's input is the features) also get their CSC."""
     import ctypes
 
     from . import _lib
@@ -205,11 +215,17 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
             M, K, nnz, ns = dims[0], dims[1], dims[2], dims[3]
             (tfr, fr), (trp, rp), (tci, ci) = buf(M + 1, torch.int32), buf(M + 1, torch.int32), buf(nnz, torch.int32)
             (tnf, nf), (tsa, sa) = buf(K, torch.float32), buf(ns, torch.int64)
-            pinned_layers.append((tfr, trp, tci, tnf))
+            tcp = tcr = cp = cr = None
+            if li >= csc_from:  # layers whose input needs a gradient: the backward's operand
+                (tcp, cp), (tcr, cr) = buf(K + 1, torch.int32), buf(nnz, torch.int32)
+            pinned_layers.append((tfr, trp, tci, tnf, tcp, tcr))
             pinned_sampled.append(tsa)
             _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, ptr(fr), ptr(rp), ptr(ci), ptr(nf), ptr(sa)),
                                "gnn_ladies_layer_copy")
-            layers.append(HostLayer(fullrowptr=fr, rowptr=rp, colidx=ci, normfact=nf, shape=(int(M), int(K))))
+            if cp is not None:
+                _lib.check_sampler(L.gnn_ladies_layer_csc(h, li, ptr(cp), ptr(cr)), "gnn_ladies_layer_csc")
+            layers.append(HostLayer(fullrowptr=fr, rowptr=rp, colidx=ci, normfact=nf, shape=(int(M), int(K)),
+                                    csc_colptr=cp, csc_rows=cr))
             sampled.append(sa)
         inp = np.empty(L.gnn_ladies_num_input_nodes(h), np.int64)
         _lib.check_sampler(L.gnn_ladies_input_nodes(h, ptr(inp)), "gnn_ladies_input_nodes")

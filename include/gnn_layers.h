@@ -41,6 +41,24 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
                           float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * fp32 GEMMs of the layers on gfx950 MFMA (gemm.hip): C[b] = A[b] · B[b] for b < nbatch
+ * (1..4 problems of one shape in one launch; A, B, C are HOST arrays of device pointers).
+ *   A(m, k) = a_kmajor ? A[k*lda + m] : A[m*lda + k]      (M x K)
+ *   B(k, n) = b_kmajor ? B[k*ldb + n] : B[n*ldb + k]      (K x N)
+ *   C(m, n) = C[m*ldc + n]                                 (M x N, row-major)
+ * Replaces the torch.nn.Linear products of GraphSageConvolution / GraphConvolution
+ * (models.py:18-21, 58-61) and their backward: forward X·Wᵀ (0, 0), input gradient G·W
+ * (0, 1), weight gradient Gᵀ·X (1, 1). Exact fp32 (each output a k-ordered fmaf chain per
+ * k-split; splits added in order: deterministic). lda, ldb even and A, B 8-byte aligned
+ * (16-byte loads when lda/ldb are multiples of 4 and the pointers 16-byte aligned). When gnn_gemm_f32_workspace_bytes(M, N, K, nbatch) > 0 the k dimension is split
+ * and `workspace` must hold that many bytes of device memory.
+ * ------------------------------------------------------------------------------- */
+size_t gnn_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch);
+int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
+                 int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
+                 size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,12 @@ int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dim
 int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fullrowptr, int32_t* rowptr,
                           int32_t* colidx, float* normfact, int64_t* sampled);
 
+/* CSC structure of layer `layer`'s sub-graph (= CSR of its transpose, canonical: rows
+ * ascending inside each column): colptr int32[K+1], rows int32[nnz]. Lets the training
+ * pipeline hand the backward aggregation its operand without a GPU transpose
+ * (custom_sparse_ops.py:34 `A.transpose(0,1).coalesce()`). */
+int gnn_ladies_layer_csc(const gnn_ladies_result* r, int32_t layer, int32_t* colptr, int32_t* rows);
+
 /* The layer-0 input node ids (the last `after`, sorted). */
 int64_t gnn_ladies_num_input_nodes(const gnn_ladies_result* r);
 int gnn_ladies_input_nodes(const gnn_ladies_result* r, int64_t* out);

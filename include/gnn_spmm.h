@@ -42,9 +42,10 @@ const char* gnn_version(void);
  *
  * X rows are read with stride ldx (elements), Y rows written with stride ldy; F <= ldx,
  * F <= ldy. Every one of the M rows of Y (columns [0, F)) is written (empty rows get 0),
- * so Y needs no zero-fill. Rows are summed in CSR order inside a work unit of `unit_nnz`
- * nonzeros; rows that straddle units are combined in unit order by a second kernel, so the
- * result is deterministic (bitwise reproducible run to run).
+ * so Y needs no zero-fill. Work is cut into units of `unit_nnz` consecutive nonzeros; a row
+ * of at most unit_nnz entries is summed whole, in CSR order, by the unit holding its first
+ * entry (bit for bit a C fmaf chain); longer rows are summed per unit and their pieces added
+ * in unit order by a second kernel — deterministic (bitwise reproducible run to run).
  *
  * `workspace` must hold gnn_spmm_workspace_bytes(M, nnz, F, unit_nnz) bytes (device
  * memory); unit_nnz <= 0 selects gnn_spmm_default_unit_nnz(M, nnz, F).
@@ -111,6 +112,16 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr,
  * Format conversions (replace the per-call preprocessing of cuda_spmm.cu:620-667 and the
  * backward's A.transpose(0,1).coalesce() of custom_sparse_ops.py:34).
  * ------------------------------------------------------------------------------- */
+
+/* Values of the TRANSPOSED operand (Aᵀ, K x M) when the caller already has A's CSC
+ * structure (colptr int32[K+1], rows int32[nnz], rows ascending inside each column — e.g.
+ * from gnn_ladies_layer_csc): val_t[i] = (float)((1.0/deg_full(rows[i])) * normfact[c]) for
+ * the entries of column c, the forward's value of the same entry bit for bit. Then
+ * (colptr, rows, val_t) is the canonical transpose (what gnn_csr_transpose builds on the GPU
+ * and custom_sparse_ops.py:34 `A.transpose(0,1).coalesce()` computes). */
+int gnn_build_operand_t_f32(const int32_t* fullrowptr, const int32_t* colptr, const int32_t* rows,
+                            const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, float* val_t,
+                            void* stream);
 
 /* Coalesced COO (int64 row and column index arrays, rows ascending) -> CSR row pointer
  * (int32, M+1) and int32 column indices. `col32` may be NULL to skip the narrowing. */

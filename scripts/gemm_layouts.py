@@ -6,8 +6,13 @@ padded K, and rocBLAS vs hipBLASLt. Prints one JSON object.
 import json
 import sys
 
+import os
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gnn_amd.fused import gemm  # noqa: E402
 
 
 def timeit(fn, reps=30):
@@ -53,9 +58,22 @@ def main():
                 "bwd_dW_padK": lambda: torch.mm(g.t(), xp),
                 "bwd_dWt": lambda: torch.mm(x.t(), g),
             }
+            if lib == "cublas":  # the hand-written MFMA kernel (library-independent)
+                xp4 = torch.zeros(M, (K + 3) // 4 * 4, device=dev)
+                xp4[:, :K] = x
+                xv = xp4[:, :K]
+                cases.update({
+                    "gnn_fwd": lambda: gemm(False, False, [x], [W], M, N, K),
+                    "gnn_fwd_pad": lambda: gemm(False, False, [xv], [W], M, N, K),
+                    "gnn_fwd_pair": lambda: gemm(False, False, [x, x], [W, W], M, N, K),
+                    "gnn_dX": lambda: gemm(False, True, [g], [W], M, K, N),
+                    "gnn_dW": lambda: gemm(True, True, [g], [x], N, K, M),
+                    "gnn_dW_pair": lambda: gemm(True, True, [g, g], [x, x], N, K, M),
+                })
             for name, fn in cases.items():
                 us = timeit(fn)
-                res[f"{lib}/{M}x{K}x{N}/{name}"] = {"us": round(us, 1), "TFLOPs": round(flops / us * 1e-6, 1)}
+                f = flops * (2 if name.endswith("_pair") else 1)
+                res[f"{lib}/{M}x{K}x{N}/{name}"] = {"us": round(us, 1), "TFLOPs": round(f / us * 1e-6, 1)}
             print(f"{lib} {M}x{K}x{N} done", file=sys.stderr, flush=True)
     print(json.dumps(res, indent=1))
 

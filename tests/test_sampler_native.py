@@ -77,6 +77,21 @@ def test_subgraph_orders(orders):
     _same(a, b)
 
 
+def test_native_csc_matches_scipy():
+    """Layers >= 1 carry their CSC (the backward operand's structure): scipy's tocsc of the
+    layer, exactly; layer 0 (input = features, no gradient) carries none."""
+    N = 5000
+    lap = _lap(N, 18, 6)
+    batch = np.random.default_rng(1).permutation(N)[:128]
+    a, _ = _both(lap, N, batch, [700] * 3, [1, 1, 1], 9)
+    assert a.layers[0].csc_colptr is None
+    for L in a.layers[1:]:
+        M, K = L.shape
+        csc = sp.csr_matrix((np.ones(L.colidx.size), L.colidx, L.rowptr), shape=(M, K)).tocsc()
+        assert np.array_equal(L.csc_colptr, csc.indptr)
+        assert np.array_equal(L.csc_rows, csc.indices)
+
+
 def test_native_exhausts_support():
     """samp_num above the number of reachable columns: s_num = #(p > 0), every one taken."""
     N = 3000

@@ -230,6 +230,27 @@ def test_build_operand_sorted_unsorted_sequence(dev):
         assert np.array_equal(op.val.cpu().numpy(), oval)
 
 
+def test_transpose_from_host_csc(dev):
+    """attach_transpose (values on the GPU from a host CSC) == the GPU transpose, bit for bit."""
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(5)
+    M, K = 700, 1500
+    lens = powerlaw_lens(M, 60, 1.3, rng, K)
+    lens[::11] = 0
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    ref = op.transpose()
+    op2 = _op(dev, full, rowptr, col, nf, M, K)
+    csc = sp.csr_matrix((np.ones(col.size), col, rowptr), shape=(M, K)).tocsc()
+    tr = cso.attach_transpose(op2, t(full), t(csc.indptr.astype(np.int32)), t(csc.indices.astype(np.int32)), t(nf))
+    torch.cuda.synchronize()
+    assert op2.transpose() is tr
+    assert torch.equal(tr.rowptr, ref.rowptr) and torch.equal(tr.col, ref.col)
+    assert torch.equal(tr.val.view(torch.int32), ref.val.view(torch.int32))
+
+
 def test_transpose_bitexact(dev):
     M, K = 3000, 2000
     rng = np.random.default_rng(9)
