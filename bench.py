@@ -392,6 +392,10 @@ def main():
                                                                         max_name_column_width=60,
                                                                         max_shapes_column_width=90))
             fh.write("\n\n")
+            fh.write(prof.key_averages().table(sort_by="count", row_limit=80, max_name_column_width=60))
+            fh.write("\n\n")
+            fh.write(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=50, max_name_column_width=60))
+            fh.write("\n\n")
             for ev in prof.events():
                 if ev.device_type.name == "CUDA":
                     continue

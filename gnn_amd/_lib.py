@@ -6,9 +6,12 @@ fallback: if the library is missing or fails to load, every operator raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
+
+import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgnn_spmm.so")
@@ -119,6 +122,22 @@ def check_sampler(rc: int, what: str) -> None:
     if rc != 0:
         msg = sampler_lib().gnn_sampler_last_error().decode(errors="replace")
         raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+_NULLCTX = contextlib.nullcontext()
+
+
+def stream_of(dev) -> int:
+    """Raw hipStream_t of torch's current stream on `dev` (no Python Stream object)."""
+    return torch._C._cuda_getCurrentRawStream(dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+def on_device(dev):
+    """torch.cuda.device(dev) only when dev is not already current (the context manager
+    costs ~10 µs a call on the host; one process per GPU keeps its device current)."""
+    if dev.index is None or dev.index == torch._C._cuda_getDevice():
+        return _NULLCTX
+    return torch.cuda.device(dev)
 
 
 def check(rc: int, what: str) -> None:

@@ -69,7 +69,7 @@ def algorithmic_bytes(M: int, nnz: int, F: int) -> int:
 
 
 def _stream(device: torch.device) -> int:
-    return torch.cuda.current_stream(device).cuda_stream
+    return _lib.stream_of(device)
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -105,7 +105,7 @@ class CsrOperand:
         if self._t is None:
             M, K = self.shape
             dev = self.device
-            with torch.cuda.device(dev):
+            with _lib.on_device(dev):
                 L = _lib.lib()
                 tr_rowptr = torch.empty(K + 1, dtype=torch.int32, device=dev)
                 tr_col = torch.empty(self.nnz, dtype=torch.int32, device=dev)
@@ -145,7 +145,7 @@ def csr_of(mat: "torch.Tensor | CsrOperand") -> CsrOperand:
     _require(M < 2**31 and K < 2**31 and nnz < 2**31, "sparseMat dims and nnz must be < 2^31")
     dev = mat.device
     idx = mat._indices()
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
         col = torch.empty(nnz, dtype=torch.int32, device=dev)
         L = _lib.lib()
@@ -197,7 +197,7 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
         avail = dense.untyped_storage().nbytes() // 4 - dense.storage_offset()
         if ldx >= F4 and (K - 1) * ldx + F4 <= avail:
             Fk = F4
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         out = torch.empty((M, Fk), dtype=torch.float32, device=dev)
         if M == 0 or F == 0:
             return out[:, :F]
@@ -283,7 +283,7 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
     colidx = colidx.contiguous()
     nnz = colidx.numel()
     dev = colidx.device
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         col32 = torch.empty(nnz, dtype=torch.int32, device=dev)
         val = torch.empty(nnz, dtype=torch.float32, device=dev)
         coo = torch.empty((2, nnz), dtype=torch.int64, device=dev) if with_coo else None
@@ -304,7 +304,7 @@ def attach_transpose(op: CsrOperand, fullrowptr: torch.Tensor, colptr: torch.Ten
     for name, t in (("colptr", colptr), ("rows", rows)):
         _require(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), f"{name} must be contiguous int32 CUDA")
     dev = op.device
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         val = torch.empty(op.nnz, dtype=torch.float32, device=dev)
         _lib.check(_lib.lib().gnn_build_operand_t_f32(_ptr(fullrowptr), _ptr(colptr), _ptr(rows), _ptr(normfact),
                                                       M, K, op.nnz, _ptr(val), _stream(dev)),
@@ -340,7 +340,7 @@ def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.T
         if t is not None:
             _require(t.is_cuda and t.dtype == torch.int64 and t.is_contiguous(), "gather_rows indices must be int64 CUDA")
     dev = dst.device
-    with torch.cuda.device(dev):
+    with _lib.on_device(dev):
         _lib.check(_lib.lib().gnn_gather_rows_f32(src.data_ptr(), src.stride(0), _ptr(src_idx), dst.data_ptr(),
                                                   dst.stride(0), _ptr(dst_idx), n, F, _stream(dev)),
                    "gnn_gather_rows_f32")

@@ -23,7 +23,7 @@ def _ptr(t: Optional[torch.Tensor]):
 
 
 def _stream(dev) -> int:
-    return torch.cuda.current_stream(dev).cuda_stream
+    return _lib.stream_of(dev)
 
 
 class SageNormFn(torch.autograd.Function):
@@ -104,6 +104,7 @@ class SageAggregateFn(torch.autograd.Function):
         xs = torch.empty((sampled.numel(), ld), dtype=x.dtype, device=x.device)[:, :F]
         cso.gather_rows(x, sampled, xs, None, n=sampled.numel())
         ctx.op = op
+        ctx.rmap = getattr(sampled, "_gnn_rmap", None)  # precomputed by HostBatch.to_device
         ctx.save_for_backward(sampled)
         return feat, xs
 
@@ -116,8 +117,10 @@ class SageAggregateFn(torch.autograd.Function):
         (sampled,) = ctx.saved_tensors
         op_t = ctx.op.transpose()
         K = op_t.shape[0]
-        rmap = torch.full((K,), -1, dtype=torch.int32, device=sampled.device)
-        rmap[sampled] = torch.arange(sampled.numel(), dtype=torch.int32, device=sampled.device)
+        rmap = ctx.rmap
+        if rmap is None or rmap.numel() != K:
+            rmap = torch.full((K,), -1, dtype=torch.int32, device=sampled.device)
+            rmap[sampled] = torch.arange(sampled.numel(), dtype=torch.int32, device=sampled.device)
         return None, cso.spmm_csr(op_t, g_feat.contiguous(), tag="bwd", residual=g_xs.contiguous(), rmap=rmap), None
 
 

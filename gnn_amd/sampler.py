@@ -70,6 +70,21 @@ class HostBatch:
                       for L in self.layers]
             sampled = [p(t(s, np.int64)) for s in self.sampled_nodes]
             self.extra["pinned"] = (layers, sampled, p(t(self.labels)))
+        if "rmaps" not in self.extra:
+            # inverse of sampled_nodes over the layer's input rows (rmap[sampled[i]] = i, -1 else):
+            # the row map of the fused backward residual (gnn_spmm_csr_f32_ex), made here so the
+            # training step launches no fill/arange/index_put for it
+            pin = torch.cuda.is_available()
+            rm = []
+            for li, (L, sn) in enumerate(zip(self.layers, self.sampled_nodes)):
+                if L is None or li == 0 or len(sn) == 0:
+                    rm.append(None)
+                    continue
+                r = np.full(L.shape[1], -1, dtype=np.int32)
+                r[np.asarray(sn, dtype=np.int64)] = np.arange(len(sn), dtype=np.int32)
+                x = torch.from_numpy(r)
+                rm.append(x.pin_memory() if pin else x)
+            self.extra["rmaps"] = rm
         return self
 
     def to_device(self, device, with_coo: bool = True, build: bool = True):
@@ -80,7 +95,11 @@ class HostBatch:
         d = lambda x: None if x is None else x.to(dev, non_blocking=True)
         raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape, d(P[4]), d(P[5]))
                for P, L in zip(layers, self.layers)]
-        db = DeviceBatch(self, raw, None, [d(s) for s in sampled], d(labels))
+        sn = [d(s) for s in sampled]
+        for x, r in zip(sn, self.extra["rmaps"]):
+            if r is not None:
+                x._gnn_rmap = d(r)  # read by fused.SageAggregateFn's backward
+        db = DeviceBatch(self, raw, None, sn, d(labels))
         if build:
             db.build_operands(with_coo=with_coo)
         return db

@@ -14,9 +14,10 @@ Here (DESIGN.md §Feature staging):
     the critical path), then one contiguous hipMemcpyAsync on a side stream, then a scatter
     kernel into X0 — the side stream runs ahead, overlapping the copy with the previous
     batch's aggregation kernels; the compute stream waits on an event only when it needs X0.
-  * Peer rows (world_size > 1): exchanged with RCCL all-to-all (``PeerExchange``): each rank
-    gathers the rows its peers asked for from its own buffer, one all_to_all_single moves
-    them over xGMI, and a scatter kernel places them.
+  * Peer rows (world_size > 1): exchanged with RCCL all-to-all (``PeerExchange``): the
+    request sizes and slot ids are negotiated on the host over a gloo group (no GPU sync),
+    each rank gathers the rows its peers asked for from its own buffer, one
+    all_to_all_single moves them over xGMI, and a scatter kernel places them.
 """
 from __future__ import annotations
 
@@ -77,6 +78,7 @@ class StagePlan:
     peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
     pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos)
+    peer_meta: Optional[tuple] = None  # PeerExchange.prepare: (send counts, recv counts, want, pos)
 
 
 def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devices=None) -> StagePlan:
@@ -121,7 +123,10 @@ class Stager:
     def issue(self, plan: StagePlan):
         dev = self.device
         st = self.stream
-        st.wait_stream(torch.cuda.current_stream(dev))  # inputs produced earlier on compute
+        if self.exchange is not None:
+            self.exchange.prepare(plan)  # host-side metadata all-to-all (gloo), in batch order
+        # No wait on the compute stream: staging only reads static buffers and its own
+        # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
             x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
             own_pos, own_src, host_pos = (t.to(dev, non_blocking=True) for t in plan.pinned)
@@ -135,11 +140,12 @@ class Stager:
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
             if len(plan.host_pos):
                 cso.gather_rows(host_dev, None, x0, host_pos, n=len(plan.host_pos))
+            extra = ()
             if self.exchange is not None:
-                self.exchange.exchange(plan, x0, self.store)
+                extra = self.exchange.exchange(plan, x0, self.store)
             ev = torch.cuda.Event()
             ev.record(st)
-        keep = (own_pos, own_src, host_pos, host_dev)
+        keep = (own_pos, own_src, host_pos, host_dev) + tuple(extra)
         return StagedX0(x0, ev, keep, self.store.F)
 
 
@@ -164,37 +170,55 @@ class PeerExchange:
     """All-to-all exchange of buffered rows held by peer GPUs (RCCL over xGMI).
 
     Rank r needs, from each peer j, the rows at slots ``plan.peer_src[j]`` of j's buffer.
-    1) all_to_all of the per-peer request counts (host-visible: sizes the next two calls),
-    2) all_to_all of the requested slot ids, 3) every rank gathers the requested rows from
-    its own buffer (HIP gather) and 4) one all_to_all_single moves the rows; 5) a scatter
-    kernel drops them at their X0 positions."""
+    ``prepare`` (host, in batch order on every rank): the per-peer request counts and the
+    requested slot ids move by two all-to-alls on a CPU (gloo) group — metadata only, so the
+    host never waits on the GPU queue. ``exchange`` (device, on the staging stream): each rank
+    gathers the rows its peers asked for from its own buffer (HIP gather), ONE RCCL
+    all_to_all_single with the sizes ``prepare`` learnt moves them over xGMI, and a scatter
+    kernel drops them at their X0 positions. Replaces the reference's per-peer P2P
+    ``gpu_buffers[i][idx].to(device)`` copies (main.py:129-133)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, meta_group=None):
         import torch.distributed as dist
 
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if meta_group is None:
+            meta_group = group if dist.get_backend(group) == "gloo" else dist.new_group(backend="gloo")
+        self.meta_group = meta_group
+
+    def prepare(self, plan: StagePlan) -> None:
+        """Host-side negotiation for one batch (idempotent). Collective: call on every rank,
+        for the same batch sequence."""
+        if getattr(plan, "peer_meta", None) is not None:
+            return
+        dist, W = self.dist, self.world
+        sc = [len(plan.peer_src[j]) for j in range(W)]
+        rc_t = torch.empty(W, dtype=torch.int64)
+        dist.all_to_all_single(rc_t, torch.tensor(sc, dtype=torch.int64), group=self.meta_group)
+        rc = rc_t.tolist()
+        req = torch.from_numpy(np.concatenate(plan.peer_src).astype(np.int64) if W else np.zeros(0, np.int64))
+        want = torch.empty(sum(rc), dtype=torch.int64)
+        dist.all_to_all_single(want, req, output_split_sizes=rc, input_split_sizes=sc, group=self.meta_group)
+        pos = torch.from_numpy(np.concatenate(plan.peer_pos).astype(np.int64) if W else np.zeros(0, np.int64))
+        pin = torch.cuda.is_available()
+        plan.peer_meta = (sc, rc, want.pin_memory() if pin else want, pos.pin_memory() if pin else pos)
 
     def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore):
-        dist = self.dist
+        self.prepare(plan)
+        sc, rc, want_h, pos_h = plan.peer_meta
         dev = x0.device
-        W = self.world
-        send_counts = torch.tensor([len(plan.peer_src[j]) for j in range(W)], dtype=torch.int64, device=dev)
-        recv_counts = torch.empty_like(send_counts)
-        dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        rc = recv_counts.cpu().tolist()  # small sync: sizes for the variable-size calls
-        sc = send_counts.cpu().tolist()
-        req = torch.from_numpy(np.concatenate(plan.peer_src) if W else np.zeros(0, np.int64)).to(dev)
-        want = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(want, req, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
-        F, ld = store.F, store.ld
+        want = want_h.to(dev, non_blocking=True)
+        pos = pos_h.to(dev, non_blocking=True)
+        ld = store.ld
         send_rows = torch.empty((sum(rc), ld), dtype=torch.float32, device=dev)
         if sum(rc):
             cso.gather_rows(store.gpu_buffer, want, send_rows, None, n=sum(rc))
         recv_rows = torch.empty((sum(sc), ld), dtype=torch.float32, device=dev)
-        dist.all_to_all_single(recv_rows, send_rows, output_split_sizes=sc, input_split_sizes=rc, group=self.group)
-        pos = torch.from_numpy(np.concatenate(plan.peer_pos) if W else np.zeros(0, np.int64)).to(dev)
+        self.dist.all_to_all_single(recv_rows, send_rows, output_split_sizes=sc, input_split_sizes=rc,
+                                    group=self.group)
         if sum(sc):
             cso.gather_rows(recv_rows, None, x0, pos, n=sum(sc))
+        return (want, pos, send_rows, recv_rows)

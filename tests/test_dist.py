@@ -3,7 +3,8 @@
 * Trainer: per-rank clip then all-reduce(SUM) of the flat gradient equals the reference's
   thread-sum semantics (main.py:146-168): grad = Σ_r clip_r(grad_r), no averaging; initial
   weights are broadcast from rank 0.
-* PeerExchange: every rank receives exactly the rows it requested from each peer's buffer.
+* PeerExchange: every rank receives exactly the rows it requested from each peer's buffer
+  (host-side negotiation of sizes and slot ids, then the row all-to-all).
 The HIP row gather is replaced by a torch index copy here (no GPU on this host).
 """
 import os
@@ -97,7 +98,10 @@ def _exchange_worker(rank, world, port, q):
     plan = staging.StagePlan(n_in, np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64),
                              torch.zeros(0, F), peer_pos, peer_src)
     x0 = torch.full((n_in, 8), -1.0)
-    staging.PeerExchange().exchange(plan, x0, store)
+    ex = staging.PeerExchange()
+    ex.prepare(plan)
+    ex.prepare(plan)  # idempotent
+    ex.exchange(plan, x0, store)
     expect = torch.arange(k * F, dtype=torch.float32).view(k, F)[torch.from_numpy(src)] + 1000 * peer
     ok = torch.equal(x0[torch.from_numpy(pos), :F], expect)
     q.put((rank, ok))
