@@ -1,0 +1,211 @@
+// optim.hip — the training step's tail in two launches: global gradient-norm clipping and
+// Adam, over all parameter tensors at once (multi-tensor: one workgroup per 8K-element chunk
+// of any tensor, the tensor list passed by value in the kernel arguments).
+//
+// Reference (main.py:146-170): clip_grad_norm_(params, 5) on each rank's gradients, the
+// per-rank sum of the clipped gradients, then torch.optim.Adam (lr, betas (0.9, 0.999),
+// eps 1e-8, no weight decay). torch runs the clip as ~6 launches (per-tensor norms, stack,
+// norm, clamp, scale) and Adam as a multi-tensor kernel that moves the 4 state streams at
+// ~1.6 TB/s; here: one partial-sum-of-squares launch + one Adam launch that finishes the
+// norm (fixed-order sum of the partials: deterministic) and applies the clip factor to the
+// gradient as it reads it.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdint>
+
+#include "common.h"
+#include "gnn_optim.h"
+
+namespace {
+
+using gnn::ceil_div;
+
+constexpr int MAXT = GNN_OPTIM_MAX_TENSORS;
+constexpr int CHUNK = 8192;  // elements per workgroup (256 threads x 8 float4)
+
+struct TensorList {
+  float* p[MAXT];
+  const float* g[MAXT];
+  float* m[MAXT];
+  float* v[MAXT];
+  int64_t n[MAXT];
+  int64_t chunk0[MAXT + 1];  // first chunk of tensor i (exclusive prefix of ceil(n / CHUNK))
+  int count;
+};
+
+__device__ __forceinline__ int tensor_of(const TensorList& L, int64_t chunk) {
+  int i = 0;
+  while (i + 1 < L.count && L.chunk0[i + 1] <= chunk) ++i;  // <= 32 entries, uniform
+  return i;
+}
+
+__device__ __forceinline__ float block_sum(float s, float* red) {
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  float t = 0.0f;
+  if (threadIdx.x == 0) t = (red[0] + red[1]) + (red[2] + red[3]);  // fixed order
+  return t;
+}
+
+// partial[chunk] = sum of squares of the gradient elements of that chunk
+__global__ __launch_bounds__(256) void grad_sqnorm_kernel(TensorList L, float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t chunk = blockIdx.x;
+  const int i = tensor_of(L, chunk);
+  const int64_t base = (chunk - L.chunk0[i]) * CHUNK;
+  const int64_t end = min(base + (int64_t)CHUNK, L.n[i]);
+  const float* g = L.g[i];
+  float s = 0.0f;
+  for (int64_t e = base + threadIdx.x; e < end; e += 256) {
+    const float x = g[e];
+    s = fmaf(x, x, s);
+  }
+  const float t = block_sum(s, red);
+  if (threadIdx.x == 0) partial[chunk] = t;
+}
+
+// scale = clip ? min(1, max_norm / (sqrt(sum partial) + 1e-6)) : 1, computed by every
+// workgroup from the same partials in the same order (no extra launch, identical result).
+__device__ float clip_scale(const float* __restrict__ partial, int64_t nchunks, float max_norm, float* red) {
+  float s = 0.0f;
+  for (int64_t c = threadIdx.x; c < nchunks; c += 256) s += partial[c];
+  const float t = block_sum(s, red);
+  __shared__ float sc;
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(t);
+    const float coef = max_norm / (norm + 1e-6f);
+    sc = coef < 1.0f ? coef : 1.0f;  // torch: clip_coef_clamped = clamp(coef, max=1)
+  }
+  __syncthreads();
+  return sc;
+}
+
+__global__ __launch_bounds__(256) void scale_into_kernel(TensorList L, const float* __restrict__ partial,
+                                                         int64_t nchunks, float max_norm, float* __restrict__ flat,
+                                                         float* __restrict__ scale_out) {
+  __shared__ float red[4];
+  const float sc = max_norm > 0.0f ? clip_scale(partial, nchunks, max_norm, red) : 1.0f;
+  const int64_t chunk = blockIdx.x;
+  if (chunk == 0 && threadIdx.x == 0 && scale_out) *scale_out = sc;
+  const int i = tensor_of(L, chunk);
+  const int64_t base = (chunk - L.chunk0[i]) * CHUNK;
+  const int64_t end = min(base + (int64_t)CHUNK, L.n[i]);
+  // flat offset of tensor i = sum of the sizes before it (its views in the flat buffer)
+  int64_t off = 0;
+  for (int j = 0; j < i; ++j) off += L.n[j];
+  for (int64_t e = base + threadIdx.x; e < end; e += 256) flat[off + e] = L.g[i][e] * sc;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(TensorList L, const float* __restrict__ partial, int64_t nchunks,
+                                                   float max_norm, float lr, float beta1, float beta2, float eps,
+                                                   float step_size, float bc2_sqrt) {
+  __shared__ float red[4];
+  const float sc = (partial && max_norm > 0.0f) ? clip_scale(partial, nchunks, max_norm, red) : 1.0f;
+  const int64_t chunk = blockIdx.x;
+  const int i = tensor_of(L, chunk);
+  const int64_t base = (chunk - L.chunk0[i]) * CHUNK;
+  const int64_t end = min(base + (int64_t)CHUNK, L.n[i]);
+  float* __restrict__ p = L.p[i];
+  const float* __restrict__ g = L.g[i];
+  float* __restrict__ m = L.m[i];
+  float* __restrict__ v = L.v[i];
+  (void)lr;
+  for (int64_t e = base + threadIdx.x; e < end; e += 256) {
+    const float gr = g[e] * sc;
+    // torch (_fused_adam / _multi_tensor_adam, amsgrad=False, weight_decay=0):
+    //   m = lerp(m, g, 1 - beta1); v = beta2 * v + (1 - beta2) * g * g
+    //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+    const float mo = m[e];
+    const float mn = mo + (1.0f - beta1) * (gr - mo);
+    const float vn = beta2 * v[e] + (1.0f - beta2) * gr * gr;
+    m[e] = mn;
+    v[e] = vn;
+    const float denom = sqrtf(vn) / bc2_sqrt + eps;
+    p[e] = p[e] - step_size * (mn / denom);
+  }
+}
+
+int fill_list(TensorList& L, int count, float* const* p, const float* const* g, float* const* m, float* const* v,
+              const int64_t* n) {
+  GNN_REQUIRE(count >= 1 && count <= MAXT, "optimizer: 1..%d tensors per call (got %d)", MAXT, count);
+  L.count = count;
+  L.chunk0[0] = 0;
+  for (int i = 0; i < count; ++i) {
+    GNN_REQUIRE(n[i] >= 0 && g[i] != nullptr, "optimizer: bad tensor %d", i);
+    L.p[i] = p ? p[i] : nullptr;
+    L.g[i] = g[i];
+    L.m[i] = m ? m[i] : nullptr;
+    L.v[i] = v ? v[i] : nullptr;
+    L.n[i] = n[i];
+    L.chunk0[i + 1] = L.chunk0[i] + ceil_div(n[i], (int64_t)CHUNK);
+  }
+  for (int i = count; i < MAXT; ++i) {
+    L.p[i] = nullptr;
+    L.g[i] = nullptr;
+    L.m[i] = nullptr;
+    L.v[i] = nullptr;
+    L.n[i] = 0;
+    L.chunk0[i + 1] = L.chunk0[count];
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t gnn_optim_chunks(int count, const int64_t* n) {
+  int64_t c = 0;
+  for (int i = 0; i < count; ++i) c += ceil_div(n[i], (int64_t)CHUNK);
+  return c;
+}
+
+int gnn_grad_sqnorm_f32(int count, const float* const* g, const int64_t* n, float* partial, void* stream) {
+  TensorList L;
+  if (int rc = fill_list(L, count, nullptr, g, nullptr, nullptr, n)) return rc;
+  const int64_t nch = L.chunk0[count];
+  GNN_REQUIRE(partial != nullptr || nch == 0, "gnn_grad_sqnorm_f32: NULL partial");
+  if (nch == 0) return 0;
+  GNN_REQUIRE(nch < INT_MAX, "gnn_grad_sqnorm_f32: too many chunks");
+  grad_sqnorm_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(L, partial);
+  GNN_LAUNCHED("grad_sqnorm_kernel");
+  return 0;
+}
+
+int gnn_clip_scale_into_f32(int count, const float* const* g, const int64_t* n, const float* partial,
+                            float max_norm, float* flat, float* scale_out, void* stream) {
+  TensorList L;
+  if (int rc = fill_list(L, count, nullptr, g, nullptr, nullptr, n)) return rc;
+  const int64_t nch = L.chunk0[count];
+  if (nch == 0) return 0;
+  GNN_REQUIRE(flat && (partial || max_norm <= 0.0f), "gnn_clip_scale_into_f32: NULL flat/partial");
+  scale_into_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(L, partial, nch, max_norm, flat,
+                                                                               scale_out);
+  GNN_LAUNCHED("scale_into_kernel");
+  return 0;
+}
+
+int gnn_adam_f32(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
+                 const int64_t* n, const float* partial, int64_t nchunks_partial, float max_norm, float lr,
+                 float beta1, float beta2, float eps, int64_t step, void* stream) {
+  TensorList L;
+  if (int rc = fill_list(L, count, p, g, m, v, n)) return rc;
+  for (int i = 0; i < count; ++i) GNN_REQUIRE(p[i] && m[i] && v[i], "gnn_adam_f32: NULL tensor %d", i);
+  GNN_REQUIRE(step >= 1, "gnn_adam_f32: step must be >= 1");
+  const int64_t nch = L.chunk0[count];
+  if (nch == 0) return 0;
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  adam_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(
+      L, partial, nchunks_partial, max_norm, lr, beta1, beta2, eps, step_size, bc2_sqrt);
+  GNN_LAUNCHED("adam_kernel");
+  return 0;
+}
+
+}  // extern "C"

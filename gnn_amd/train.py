@@ -4,12 +4,14 @@ Reference: per-rank threads in one process; grads flattened with torch.cat, publ
 shared list, ``threading.Barrier``, summed with P2P ``.to(device)`` copies (main.py:149-168);
 per-rank clip_grad_norm_(5) BEFORE the sum and no averaging (main.py:146,159).
 
-Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). After
-the per-rank clip, the gradients are packed into one flat fp32 buffer (a single copy
-kernel), summed with ONE in-place ``all_reduce(SUM)``, and handed back to the parameters as
-views of that buffer (no copy back). Gradients are reset to None each step, so autograd
-hands its freshly computed tensors over instead of accumulating into old ones. Initial
-weights are broadcast from rank 0 (the reference never syncs them: SURVEY.md Appendix B, F).
+Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). On the
+GPU the per-rank clip writes the clipped gradients straight into one flat fp32 buffer (one
+kernel, gnn_amd.optim), summed with ONE in-place ``all_reduce(SUM)``, and Adam reads them as
+views of that buffer; at N = 1 the clip factor is applied inside the Adam launch. (On the CPU
+— the gloo tests — the same semantics run through torch's clip_grad_norm_ and Adam.)
+Gradients are reset to None each step, so autograd hands its freshly computed tensors over
+instead of accumulating into old ones. Initial weights are broadcast from rank 0 (the
+reference never syncs them: SURVEY.md Appendix B, F).
 """
 from __future__ import annotations
 
@@ -30,14 +32,18 @@ class Trainer:
         self.clip = clip
         self.group = group
         self.params = [p for p in model.parameters() if p.requires_grad]
-        # One fused multi-tensor kernel on the GPU instead of the foreach kernel chain (same
-        # Adam update; the reference's default Adam, main.py:102).
-        fused = self.device.type == "cuda"
-        if fused:
+        # The reference's default Adam (main.py:102) and clip_grad_norm_(5) (main.py:146).
+        self.native = self.device.type == "cuda"
+        if self.native:
             # The layer GEMMs (15k x 602..1024 x 512, fp32): rocBLAS ("cublas" on ROCm builds)
             # measured faster than hipBLASLt on MI355X (317 vs 294 mini-batches/s, same box).
             torch.backends.cuda.preferred_blas_library("cublas")
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, fused=fused)
+            # clip + Adam in two HIP launches (gnn_amd.optim, include/gnn_optim.h)
+            from .optim import ClipAdam
+
+            self.optimizer = ClipAdam(self.params, lr=lr, max_norm=clip)
+        else:
+            self.optimizer = torch.optim.Adam(self.params, lr=lr)
         self.world = 1
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world = torch.distributed.get_world_size(group)
@@ -73,6 +79,14 @@ class Trainer:
         out = self.model(x0, adjs, sampled_nodes)
         loss = loss_fn(out, labels, self.sigmoid_loss, self.device)
         loss.backward()
+        if self.native:
+            if self.world > 1:
+                flat = self.optimizer.clip_to_flat()  # this rank's clip, into the all-reduce buffer
+                torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
+                self.optimizer.step(clipped=True)
+            else:
+                self.optimizer.step()  # clip applied inside the Adam launch
+            return loss.detach()
         torch.nn.utils.clip_grad_norm_(self.params, self.clip)
         self.allreduce_grads()
         self.optimizer.step()
