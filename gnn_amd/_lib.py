@@ -39,6 +39,7 @@ _SIGNATURES = {
     "gnn_segsort_workspace_bytes": (_SZ, [_I64]),
     "gnn_build_operand_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
     "gnn_build_operand_t_f32": (_INT, [_VP, _VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP]),
+    "gnn_build_operand_sorted_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP]),
     "gnn_coo_to_csr": (_INT, [_VP, _VP, _I64, _I64, _VP, _VP, _VP]),
     "gnn_csr_transpose_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "gnn_csr_transpose": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),

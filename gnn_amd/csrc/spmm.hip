@@ -1220,10 +1220,35 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
 
 size_t gnn_segsort_workspace_bytes(int64_t nseg) { return segsort_ws(nseg); }
 
+namespace {
+int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
+                  const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col, float* csr_val,
+                  int64_t* coo_indices, bool sorted, void* stream);
+}  // namespace
+
 int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
                           const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col,
                           float* csr_val, int64_t* coo_indices, void* workspace, size_t workspace_bytes,
                           void* stream) {
+  (void)workspace;  // not needed (the unsorted-row flag lives in the library); ABI stability
+  (void)workspace_bytes;
+  return build_operand(fullrowptr, rowptr, colidx, colidx_bytes, normfact, nrows, ncols, nnz, csr_col, csr_val,
+                       coo_indices, false, stream);
+}
+
+int gnn_build_operand_sorted_f32(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx,
+                                 int colidx_bytes, const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz,
+                                 int32_t* csr_col, float* csr_val, int64_t* coo_indices, void* stream) {
+  return build_operand(fullrowptr, rowptr, colidx, colidx_bytes, normfact, nrows, ncols, nnz, csr_col, csr_val,
+                       coo_indices, true, stream);
+}
+
+}  // extern "C"
+
+namespace {
+int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
+                  const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col, float* csr_val,
+                  int64_t* coo_indices, bool sorted, void* stream) {
   GNN_REQUIRE(nrows >= 0 && ncols >= 0 && nnz >= 0, "gnn_build_operand_f32: negative size");
   GNN_REQUIRE(nrows < INT_MAX && ncols < INT_MAX && nnz < INT_MAX, "gnn_build_operand_f32: sizes must be < 2^31");
   GNN_REQUIRE(colidx_bytes == 2 || colidx_bytes == 4 || colidx_bytes == 8,
@@ -1232,8 +1257,6 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
   GNN_REQUIRE(fullrowptr && rowptr && colidx && normfact && csr_col && csr_val, "gnn_build_operand_f32: NULL input");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)ceil_div(nrows, 4));
-  (void)workspace;  // not needed (the unsorted-row flag lives in the library); ABI stability
-  (void)workspace_bytes;
   unsigned long long* flag = nullptr;
   unsigned long long gen = 0;
   if (int rc = operand_flag(&flag, &gen)) return rc;
@@ -1244,21 +1267,24 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
       build_operand_flat_kernel<int16_t><<<gflat, dim3(256), 0, st>>>(
           fullrowptr, rowptr, (const int16_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
       GNN_LAUNCHED("build_operand_flat_kernel");
-      build_operand_kernel<int16_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
+      if (!sorted)
+        build_operand_kernel<int16_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int16_t*)colidx, normfact,
                                                                 (int)nrows, csr_col, csr_val, flag, gen);
       break;
     case 4:
       build_operand_flat_kernel<int32_t><<<gflat, dim3(256), 0, st>>>(
           fullrowptr, rowptr, (const int32_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
       GNN_LAUNCHED("build_operand_flat_kernel");
-      build_operand_kernel<int32_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
+      if (!sorted)
+        build_operand_kernel<int32_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int32_t*)colidx, normfact,
                                                                 (int)nrows, csr_col, csr_val, flag, gen);
       break;
     default:
       build_operand_flat_kernel<int64_t><<<gflat, dim3(256), 0, st>>>(
           fullrowptr, rowptr, (const int64_t*)colidx, normfact, (int)nrows, (int)nnz, csr_col, csr_val, flag, gen);
       GNN_LAUNCHED("build_operand_flat_kernel");
-      build_operand_kernel<int64_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
+      if (!sorted)
+        build_operand_kernel<int64_t><<<gfix, dim3(256), 0, st>>>(fullrowptr, rowptr, (const int64_t*)colidx, normfact,
                                                                 (int)nrows, csr_col, csr_val, flag, gen);
       break;
   }
@@ -1269,6 +1295,9 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
   }
   return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int gnn_build_operand_t_f32(const int32_t* fullrowptr, const int32_t* colptr, const int32_t* rows,
                             const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, float* val_t,

@@ -270,8 +270,10 @@ spmm_naive = spmm_load_balance
 
 
 def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.Tensor, normfact: torch.Tensor,
-                  nrows: int, ncols: int, with_coo: bool = True):
-    """Device operand from the sampler's CSR pieces. Returns (CsrOperand, coo_indices|None)."""
+                  nrows: int, ncols: int, with_coo: bool = True, sorted_rows: bool = False):
+    """Device operand from the sampler's CSR pieces. Returns (CsrOperand, coo_indices|None).
+    sorted_rows=True: the caller guarantees column-ascending rows (the native samplers' output)
+    and the unsorted-row pass is not launched."""
     for name, t in (("fullrowptr", fullrowptr), ("rowptr", rowptr), ("normfact", normfact)):
         _require(t.is_cuda, f"{name} must be a CUDA tensor")
         _require(t.is_contiguous(), f"{name} must be contiguous")
@@ -287,10 +289,15 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
         col32 = torch.empty(nnz, dtype=torch.int32, device=dev)
         val = torch.empty(nnz, dtype=torch.float32, device=dev)
         coo = torch.empty((2, nnz), dtype=torch.int64, device=dev) if with_coo else None
-        _lib.check(_lib.lib().gnn_build_operand_f32(
-            _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
-            nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), None, 0, _stream(dev)),
-            "gnn_build_operand_f32")
+        if sorted_rows:
+            _lib.check(_lib.lib().gnn_build_operand_sorted_f32(
+                _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
+                nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _stream(dev)), "gnn_build_operand_sorted_f32")
+        else:
+            _lib.check(_lib.lib().gnn_build_operand_f32(
+                _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
+                nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), None, 0, _stream(dev)),
+                "gnn_build_operand_f32")
     return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
 
 

@@ -124,7 +124,8 @@ class DeviceBatch:
                 adjs.append(None)
                 continue
             fr, rp, ci, nf, shape, cp, cr = r
-            op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo)
+            op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo,
+                                        sorted_rows=bool(self.host.extra.get("sorted_rows", False)))
             if cp is not None:  # host-made CSC: the backward's operand without a GPU transpose
                 cso.attach_transpose(op, fr, cp, cr, nf)
             if with_coo:
@@ -273,6 +274,7 @@ def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, 
                            idx_of_nodes_on_device, devices, seed)
         lab = torch.from_numpy(hb.labels)
         hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        hb.extra["sorted_rows"] = True  # native samplers emit column-ascending rows by construction
         return hb
     if isinstance(lap_matrix, NativeGraph):
         lap_matrix = lap_matrix.lap
@@ -359,6 +361,7 @@ def subgraph_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix
                            idx_of_nodes_on_device, devices, seed)
         lab = torch.from_numpy(hb.labels)
         hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        hb.extra["sorted_rows"] = True  # native samplers emit column-ascending rows by construction
         return hb
     if isinstance(lap_matrix, NativeGraph):
         lap_matrix = lap_matrix.lap
@@ -434,6 +437,7 @@ def fastgcn_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix,
                            idx_of_nodes_on_device, devices, seed)
         lab = torch.from_numpy(hb.labels)
         hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
+        hb.extra["sorted_rows"] = True  # native samplers emit column-ascending rows by construction
         return hb
     lap = g.lap
     p = g.fastgcn_p

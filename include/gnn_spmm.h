@@ -108,6 +108,13 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr,
                           int32_t* csr_col, float* csr_val, int64_t* coo_indices,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* Same, for rows the caller guarantees column-ascending (e.g. gnn_ladies_sample output): no
+ * unsorted-row check pass is launched (one launch instead of two). */
+int gnn_build_operand_sorted_f32(const int32_t* fullrowptr, const int32_t* rowptr,
+                                 const void* colidx, int colidx_bytes,
+                                 const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz,
+                                 int32_t* csr_col, float* csr_val, int64_t* coo_indices, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Format conversions (replace the per-call preprocessing of cuda_spmm.cu:620-667 and the
  * backward's A.transpose(0,1).coalesce() of custom_sparse_ops.py:34).

@@ -221,6 +221,10 @@ def test_build_operand_sorted_unsorted_sequence(dev):
     for r in range(0, M, 3):
         rng.shuffle(shuffled[rowptr[r]:rowptr[r + 1]])
     ocol, oval = O.build_operand(full, rowptr, col, nf)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    fast, _ = cso.build_operand(t(full), t(rowptr), t(col), t(nf), M, K, with_coo=False, sorted_rows=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(fast.col.cpu().numpy(), ocol) and np.array_equal(fast.val.cpu().numpy(), oval)
     side = torch.cuda.Stream(device=dev)
     for c, st in ((shuffled, None), (col, None), (shuffled, side), (col, side), (shuffled, None)):
         with torch.cuda.stream(st if st is not None else torch.cuda.current_stream(dev)):
