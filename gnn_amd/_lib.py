@@ -54,9 +54,10 @@ _SIGNATURES = {
     # include/gnn_optim.h
     "gnn_optim_chunks": (_I64, [_INT, _VP]),
     "gnn_grad_sqnorm_f32": (_INT, [_INT, _VP, _VP, _VP, _VP]),
-    "gnn_clip_scale_into_f32": (_INT, [_INT, _VP, _VP, _VP, ctypes.c_float, _VP, _VP, _VP]),
-    "gnn_adam_f32": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float,
-                            ctypes.c_float, ctypes.c_float, ctypes.c_float, _I64, _VP]),
+    "gnn_clip_scale_f32": (_INT, [_VP, _I64, ctypes.c_float, _VP, _VP]),
+    "gnn_scale_into_f32": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),
+    "gnn_adam_f32": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                            ctypes.c_float, _I64, _VP]),
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
 }

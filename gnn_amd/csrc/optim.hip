@@ -1,14 +1,14 @@
-// optim.hip — the training step's tail in two launches: global gradient-norm clipping and
-// Adam, over all parameter tensors at once (multi-tensor: one workgroup per 8K-element chunk
+// optim.hip — the training step's tail in three launches: global gradient-norm clipping and
+// Adam, over all parameter tensors at once (multi-tensor: one workgroup per 1K-element chunk
 // of any tensor, the tensor list passed by value in the kernel arguments).
 //
 // Reference (main.py:146-170): clip_grad_norm_(params, 5) on each rank's gradients, the
 // per-rank sum of the clipped gradients, then torch.optim.Adam (lr, betas (0.9, 0.999),
 // eps 1e-8, no weight decay). torch runs the clip as ~6 launches (per-tensor norms, stack,
 // norm, clamp, scale) and Adam as a multi-tensor kernel that moves the 4 state streams at
-// ~1.6 TB/s; here: one partial-sum-of-squares launch + one Adam launch that finishes the
-// norm (fixed-order sum of the partials: deterministic) and applies the clip factor to the
-// gradient as it reads it.
+// ~1.6 TB/s; here: a partial-sum-of-squares launch, a one-workgroup launch that turns the
+// partials into the clip factor (fixed-order sum: deterministic), and one Adam launch that
+// applies the factor to the gradient as it reads it.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -23,7 +23,7 @@ namespace {
 using gnn::ceil_div;
 
 constexpr int MAXT = GNN_OPTIM_MAX_TENSORS;
-constexpr int CHUNK = 8192;  // elements per workgroup (256 threads x 8 float4)
+constexpr int CHUNK = 1024;  // elements per workgroup: 4 per thread, enough workgroups to fill the chip
 
 struct TensorList {
   float* p[MAXT];
@@ -68,29 +68,24 @@ __global__ __launch_bounds__(256) void grad_sqnorm_kernel(TensorList L, float* _
   if (threadIdx.x == 0) partial[chunk] = t;
 }
 
-// scale = clip ? min(1, max_norm / (sqrt(sum partial) + 1e-6)) : 1, computed by every
-// workgroup from the same partials in the same order (no extra launch, identical result).
-__device__ float clip_scale(const float* __restrict__ partial, int64_t nchunks, float max_norm, float* red) {
+// scale = min(1, max_norm / (sqrt(sum partial) + 1e-6)) (torch: clip_coef clamped to 1), one
+// workgroup, partials summed in a fixed order.
+__global__ __launch_bounds__(256) void clip_scale_kernel(const float* __restrict__ partial, int64_t nchunks,
+                                                         float max_norm, float* __restrict__ scale) {
+  __shared__ float red[4];
   float s = 0.0f;
   for (int64_t c = threadIdx.x; c < nchunks; c += 256) s += partial[c];
   const float t = block_sum(s, red);
-  __shared__ float sc;
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(t);
-    const float coef = max_norm / (norm + 1e-6f);
-    sc = coef < 1.0f ? coef : 1.0f;  // torch: clip_coef_clamped = clamp(coef, max=1)
+    const float coef = max_norm / (sqrtf(t) + 1e-6f);
+    *scale = coef < 1.0f ? coef : 1.0f;
   }
-  __syncthreads();
-  return sc;
 }
 
-__global__ __launch_bounds__(256) void scale_into_kernel(TensorList L, const float* __restrict__ partial,
-                                                         int64_t nchunks, float max_norm, float* __restrict__ flat,
-                                                         float* __restrict__ scale_out) {
-  __shared__ float red[4];
-  const float sc = max_norm > 0.0f ? clip_scale(partial, nchunks, max_norm, red) : 1.0f;
+__global__ __launch_bounds__(256) void scale_into_kernel(TensorList L, const float* __restrict__ scale,
+                                                         float* __restrict__ flat) {
+  const float sc = scale ? *scale : 1.0f;
   const int64_t chunk = blockIdx.x;
-  if (chunk == 0 && threadIdx.x == 0 && scale_out) *scale_out = sc;
   const int i = tensor_of(L, chunk);
   const int64_t base = (chunk - L.chunk0[i]) * CHUNK;
   const int64_t end = min(base + (int64_t)CHUNK, L.n[i]);
@@ -100,11 +95,9 @@ __global__ __launch_bounds__(256) void scale_into_kernel(TensorList L, const flo
   for (int64_t e = base + threadIdx.x; e < end; e += 256) flat[off + e] = L.g[i][e] * sc;
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(TensorList L, const float* __restrict__ partial, int64_t nchunks,
-                                                   float max_norm, float lr, float beta1, float beta2, float eps,
-                                                   float step_size, float bc2_sqrt) {
-  __shared__ float red[4];
-  const float sc = (partial && max_norm > 0.0f) ? clip_scale(partial, nchunks, max_norm, red) : 1.0f;
+__global__ __launch_bounds__(256) void adam_kernel(TensorList L, const float* __restrict__ scale, float beta1,
+                                                   float beta2, float eps, float step_size, float bc2_sqrt) {
+  const float sc = scale ? *scale : 1.0f;
   const int64_t chunk = blockIdx.x;
   const int i = tensor_of(L, chunk);
   const int64_t base = (chunk - L.chunk0[i]) * CHUNK;
@@ -113,7 +106,6 @@ __global__ __launch_bounds__(256) void adam_kernel(TensorList L, const float* __
   const float* __restrict__ g = L.g[i];
   float* __restrict__ m = L.m[i];
   float* __restrict__ v = L.v[i];
-  (void)lr;
   for (int64_t e = base + threadIdx.x; e < end; e += 256) {
     const float gr = g[e] * sc;
     // torch (_fused_adam / _multi_tensor_adam, amsgrad=False, weight_decay=0):
@@ -176,34 +168,43 @@ int gnn_grad_sqnorm_f32(int count, const float* const* g, const int64_t* n, floa
   return 0;
 }
 
-int gnn_clip_scale_into_f32(int count, const float* const* g, const int64_t* n, const float* partial,
-                            float max_norm, float* flat, float* scale_out, void* stream) {
+int gnn_clip_scale_f32(const float* partial, int64_t nchunks, float max_norm, float* scale, void* stream) {
+  GNN_REQUIRE(scale != nullptr && (partial != nullptr || nchunks == 0), "gnn_clip_scale_f32: NULL argument");
+  GNN_REQUIRE(max_norm > 0.0f, "gnn_clip_scale_f32: max_norm must be > 0");
+  clip_scale_kernel<<<dim3(1), dim3(256), 0, (hipStream_t)stream>>>(partial, nchunks, max_norm, scale);
+  GNN_LAUNCHED("clip_scale_kernel");
+  return 0;
+}
+
+int gnn_scale_into_f32(int count, const float* const* g, const int64_t* n, const float* scale, float* flat,
+                       void* stream) {
   TensorList L;
   if (int rc = fill_list(L, count, nullptr, g, nullptr, nullptr, n)) return rc;
   const int64_t nch = L.chunk0[count];
   if (nch == 0) return 0;
-  GNN_REQUIRE(flat && (partial || max_norm <= 0.0f), "gnn_clip_scale_into_f32: NULL flat/partial");
-  scale_into_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(L, partial, nch, max_norm, flat,
-                                                                               scale_out);
+  GNN_REQUIRE(flat != nullptr, "gnn_scale_into_f32: NULL flat");
+  GNN_REQUIRE(nch < INT_MAX, "gnn_scale_into_f32: too many chunks");
+  scale_into_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(L, scale, flat);
   GNN_LAUNCHED("scale_into_kernel");
   return 0;
 }
 
 int gnn_adam_f32(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
-                 const int64_t* n, const float* partial, int64_t nchunks_partial, float max_norm, float lr,
-                 float beta1, float beta2, float eps, int64_t step, void* stream) {
+                 const int64_t* n, const float* scale, float lr, float beta1, float beta2, float eps, int64_t step,
+                 void* stream) {
   TensorList L;
   if (int rc = fill_list(L, count, p, g, m, v, n)) return rc;
   for (int i = 0; i < count; ++i) GNN_REQUIRE(p[i] && m[i] && v[i], "gnn_adam_f32: NULL tensor %d", i);
   GNN_REQUIRE(step >= 1, "gnn_adam_f32: step must be >= 1");
   const int64_t nch = L.chunk0[count];
   if (nch == 0) return 0;
+  GNN_REQUIRE(nch < INT_MAX, "gnn_adam_f32: too many chunks");
   const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
   const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
   const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)std::sqrt(bc2);
-  adam_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(
-      L, partial, nchunks_partial, max_norm, lr, beta1, beta2, eps, step_size, bc2_sqrt);
+  adam_kernel<<<dim3((unsigned)nch), dim3(256), 0, (hipStream_t)stream>>>(L, scale, beta1, beta2, eps, step_size,
+                                                                         bc2_sqrt);
   GNN_LAUNCHED("adam_kernel");
   return 0;
 }

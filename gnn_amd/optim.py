@@ -40,6 +40,7 @@ class ClipAdam:
         self.nchunks = sum(self._chunks)
         dev = self.params[0].device
         self.partial = torch.empty(max(self.nchunks, 1), dtype=torch.float32, device=dev)
+        self.scale = torch.ones(1, dtype=torch.float32, device=dev)  # the clip factor (device)
         self._p = [_arr([self.params[i].data_ptr() for i in g]) for g in self.groups]
         self._m = [_arr([self.m[i].data_ptr() for i in g]) for g in self.groups]
         self._v = [_arr([self.v[i].data_ptr() for i in g]) for g in self.groups]
@@ -58,13 +59,16 @@ class ClipAdam:
             gs.append(g)
         return gs
 
-    def _norm_partials(self, gs, st):
+    def _clip_scale(self, gs, st):
+        """Partial sums of squares per chunk, then the clip factor into self.scale."""
         L = _lib.lib()
         off = 0
         for g, n, c in zip(self.groups, self._n, self._chunks):
             _lib.check(L.gnn_grad_sqnorm_f32(len(g), _arr([gs[i].data_ptr() for i in g]), n,
                                              self.partial.data_ptr() + 4 * off, st), "gnn_grad_sqnorm_f32")
             off += c
+        _lib.check(L.gnn_clip_scale_f32(self.partial.data_ptr(), self.nchunks, self.max_norm, self.scale.data_ptr(),
+                                        st), "gnn_clip_scale_f32")
 
     def clip_to_flat(self) -> torch.Tensor:
         """Per-rank clip, written into a new flat buffer (the all-reduce input); the
@@ -72,16 +76,17 @@ class ClipAdam:
         gs = self._grads()
         dev = self.params[0].device
         st = _lib.stream_of(dev)
-        self._norm_partials(gs, st)
+        scale = None
+        if self.max_norm > 0:
+            self._clip_scale(gs, st)
+            scale = self.scale.data_ptr()
         flat = torch.empty(self.numel, dtype=torch.float32, device=dev)
         L = _lib.lib()
         base = 0
         for g, n in zip(self.groups, self._n):
-            cnt = sum(self.params[i].numel() for i in g)
-            _lib.check(L.gnn_clip_scale_into_f32(len(g), _arr([gs[i].data_ptr() for i in g]), n,
-                                                 self.partial.data_ptr(), self.max_norm,
-                                                 flat.data_ptr() + 4 * base, None, st), "gnn_clip_scale_into_f32")
-            base += cnt
+            _lib.check(L.gnn_scale_into_f32(len(g), _arr([gs[i].data_ptr() for i in g]), n, scale,
+                                            flat.data_ptr() + 4 * base, st), "gnn_scale_into_f32")
+            base += sum(self.params[i].numel() for i in g)
         off = 0
         for p in self.params:
             p.grad = flat[off:off + p.numel()].view_as(p)
@@ -95,12 +100,12 @@ class ClipAdam:
         dev = self.params[0].device
         st = _lib.stream_of(dev)
         L = _lib.lib()
+        scale = None
         if not clipped and self.max_norm > 0:
-            self._norm_partials(gs, st)
+            self._clip_scale(gs, st)
+            scale = self.scale.data_ptr()
         self.step_count += 1
         b1, b2 = self.betas
         for g, n, pp, mm, vv in zip(self.groups, self._n, self._p, self._m, self._v):
-            part = None if clipped or self.max_norm <= 0 else self.partial.data_ptr()
-            _lib.check(L.gnn_adam_f32(len(g), pp, _arr([gs[i].data_ptr() for i in g]), mm, vv, n, part,
-                                      self.nchunks, self.max_norm, self.lr, b1, b2, self.eps, self.step_count, st),
-                       "gnn_adam_f32")
+            _lib.check(L.gnn_adam_f32(len(g), pp, _arr([gs[i].data_ptr() for i in g]), mm, vv, n, scale, self.lr, b1,
+                                      b2, self.eps, self.step_count, st), "gnn_adam_f32")

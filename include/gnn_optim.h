@@ -6,12 +6,12 @@
  * semantics are kept: the clip uses the rank's own gradients (before the cross-rank sum),
  * the gradients are summed (not averaged) across ranks, Adam is torch's (amsgrad off, no
  * weight decay). Tensors are passed as HOST arrays of device pointers (count <= 32 per
- * call); n[i] = element count. Partial sums are per 8192-element chunk:
+ * call); n[i] = element count. Partial sums are per 1024-element chunk:
  * gnn_optim_chunks(count, n) floats of device workspace.
  *
- *  N = 1:  gnn_grad_sqnorm_f32  ->  gnn_adam_f32(partial, max_norm)   (clip applied inside)
- *  N > 1:  gnn_grad_sqnorm_f32  ->  gnn_clip_scale_into_f32 (clipped grads into the flat
- *          all-reduce buffer)  ->  all-reduce(SUM)  ->  gnn_adam_f32(partial = NULL) on the
+ *  N = 1:  gnn_grad_sqnorm_f32 -> gnn_clip_scale_f32 -> gnn_adam_f32(scale)   (clip inside)
+ *  N > 1:  gnn_grad_sqnorm_f32 -> gnn_clip_scale_f32 -> gnn_scale_into_f32 (clipped grads into
+ *          the flat all-reduce buffer) -> all-reduce(SUM) -> gnn_adam_f32(scale = NULL) on the
  *          flat buffer's views.
  */
 #ifndef GNN_OPTIM_H
@@ -31,17 +31,18 @@ int64_t gnn_optim_chunks(int count, const int64_t* n);
 /* partial[c] = sum of g^2 over chunk c (fixed order inside the chunk). */
 int gnn_grad_sqnorm_f32(int count, const float* const* g, const int64_t* n, float* partial, void* stream);
 
-/* flat[off_i + e] = g_i[e] * min(1, max_norm / (||g|| + 1e-6)) (max_norm <= 0: no clip);
- * off_i = sum of n before i. scale_out (device float, may be NULL) receives the factor. */
-int gnn_clip_scale_into_f32(int count, const float* const* g, const int64_t* n, const float* partial,
-                            float max_norm, float* flat, float* scale_out, void* stream);
+/* *scale = min(1, max_norm / (sqrt(sum of the nchunks partials) + 1e-6)); max_norm > 0. */
+int gnn_clip_scale_f32(const float* partial, int64_t nchunks, float max_norm, float* scale, void* stream);
 
-/* One Adam step (torch semantics, step = 1-based count) with the gradient scaled by the clip
- * factor computed from `partial` (nchunks_partial entries) when partial != NULL and
- * max_norm > 0. */
+/* flat[off_i + e] = g_i[e] * (*scale) (scale may be NULL: 1); off_i = sum of n before i. */
+int gnn_scale_into_f32(int count, const float* const* g, const int64_t* n, const float* scale, float* flat,
+                       void* stream);
+
+/* One Adam step (torch semantics, step = 1-based count), the gradient multiplied by *scale
+ * (device float; NULL = 1) as it is read. */
 int gnn_adam_f32(int count, float* const* p, const float* const* g, float* const* m, float* const* v,
-                 const int64_t* n, const float* partial, int64_t nchunks_partial, float max_norm, float lr,
-                 float beta1, float beta2, float eps, int64_t step, void* stream);
+                 const int64_t* n, const float* scale, float lr, float beta1, float beta2, float eps, int64_t step,
+                 void* stream);
 
 #ifdef __cplusplus
 }
