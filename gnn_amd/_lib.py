@@ -58,6 +58,10 @@ _SIGNATURES = {
     "gnn_scale_into_f32": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP]),
     "gnn_adam_f32": (_INT, [_INT, _VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                             ctypes.c_float, _I64, _VP]),
+    "gnn_head_bce_fwd_f32": (_INT, [_VP, _I64, _I64, _I64, _VP, _VP, _I64, _VP, _I64, ctypes.c_float,
+                                    ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _VP, _VP]),
+    "gnn_head_bce_bwd_f32": (_INT, [_VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _VP, ctypes.c_float,
+                                    ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _I64, _VP]),
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
 }

@@ -318,3 +318,73 @@ def sage_norm(hB: Optional[torch.Tensor], hW: torch.Tensor, scale: torch.Tensor,
     their gradients reduced, inside the fused kernels."""
     seed = int(torch.randint(0, 2**62, (1,)).item()) if (training and p > 0) else 0
     return SageNormFn.apply(hB, hW, scale, offset, biasB, biasW, float(p), bool(training and p > 0), seed)
+
+
+class HeadBCEFn(torch.autograd.Function):
+    """GNN's head and loss (models.py:90-97 + utils.py:129-140, sigmoid_loss):
+    BCEWithLogits(linear(dropout(normalize(x))), labels, weight 1/M, "sum") in one HIP pass
+    (gnn_head_bce_fwd_f32) + a fixed-order row sum; backward one HIP pass for dx and dz, then
+    dW = dzᵀ·xd (C x D, a small GEMM) and db = Σ_rows dz. Returns (loss, logits)."""
+
+    @staticmethod
+    def forward(ctx, x, W, b, labels, p: float, training: bool, seed: int):
+        M, D = x.shape
+        C = W.shape[0]
+        dev = x.device
+        W = W.contiguous()
+        b = b.contiguous() if b is not None else None
+        labels = labels if (labels.dim() == 2 and labels.stride(1) == 1) else labels.contiguous()
+        if labels.dtype != torch.float32:
+            labels = labels.float()
+        xd = torch.empty((M, D), dtype=torch.float32, device=dev)
+        z = torch.empty((M, C), dtype=torch.float32, device=dev)
+        nrm = torch.empty(M, dtype=torch.float32, device=dev)
+        rowloss = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        _lib.check(_lib.lib().gnn_head_bce_fwd_f32(x.data_ptr(), x.stride(0), M, D, W.data_ptr(), _ptr(b), C,
+                                                   labels.data_ptr(), labels.stride(0), float(p), seed,
+                                                   int(training), xd.data_ptr(), z.data_ptr(), nrm.data_ptr(),
+                                                   rowloss.data_ptr(), loss.data_ptr(), _stream(dev)),
+                   "gnn_head_bce_fwd_f32")
+        ctx.save_for_backward(x, W, labels, xd, z, nrm)
+        ctx.cfg = (float(p), int(training), int(seed), b is not None)
+        ctx.mark_non_differentiable(z)
+        return loss, z
+
+    @staticmethod
+    def backward(ctx, gloss, _gz):
+        x, W, labels, xd, z, nrm = ctx.saved_tensors
+        p, training, seed, has_bias = ctx.cfg
+        M, D = x.shape
+        C = W.shape[0]
+        dev = x.device
+        gloss = gloss.contiguous()
+        dz = torch.empty((M, C), dtype=torch.float32, device=dev)
+        dx = torch.empty((M, D), dtype=torch.float32, device=dev)
+        _lib.check(_lib.lib().gnn_head_bce_bwd_f32(x.data_ptr(), x.stride(0), M, D, W.data_ptr(), C,
+                                                   labels.data_ptr(), labels.stride(0), gloss.data_ptr(), p, seed,
+                                                   training, z.data_ptr(), nrm.data_ptr(), dz.data_ptr(),
+                                                   dx.data_ptr(), D, _stream(dev)),
+                   "gnn_head_bce_bwd_f32")
+        dW = torch.mm(dz.t(), xd) if ctx.needs_input_grad[1] else None
+        db = dz.sum(0) if (has_bias and ctx.needs_input_grad[2]) else None
+        return dx, dW, db, None, None, None, None
+
+
+def head_supported(x: torch.Tensor, W: torch.Tensor, labels: torch.Tensor) -> bool:
+    M, D = x.shape
+    return (x.is_cuda and x.dtype == torch.float32 and W.dtype == torch.float32 and x.stride(1) == 1
+            and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and D % 4 == 0 and D <= 2048
+            and W.shape[0] <= 64 and labels.shape == (M, W.shape[0]))
+
+
+def head_bce_loss(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], labels: torch.Tensor,
+                  p: float = 0.0, training: bool = False):
+    """(loss, logits) of GNN's head with the sigmoid loss — see HeadBCEFn. Raises when the
+    operands are outside the kernel's contract (callers check head_supported first)."""
+    if not head_supported(x, W, labels):
+        raise RuntimeError("head_bce_loss: fp32 CUDA x (M x D, D % 4 == 0, D <= 2048, 16-byte rows), "
+                           "at most 64 classes, labels M x C")
+    tr = bool(training and p > 0)
+    seed = int(torch.randint(0, 2**62, (1,)).item()) if tr else 0
+    return HeadBCEFn.apply(x, W, b, labels, float(p), tr, seed)

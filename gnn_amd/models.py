@@ -155,6 +155,20 @@ class GNN(nn.Module):
         x = self.linear(x)
         return x
 
+    def forward_loss(self, feat, adjs, sampled_nodes, labels, sigmoid_loss: bool = True):
+        """(loss, logits) = (utils.loss(forward(...), labels), forward(...)). With the fused
+        GPU encoder and the sigmoid loss, the head (normalize, dropout, linear) and the BCE run
+        as one HIP pass each way (gnn_amd.fused.head_bce_loss); otherwise as the modules above."""
+        x = self.encoder(feat, adjs, sampled_nodes)
+        if sigmoid_loss and getattr(self.encoder, "fused", False) and x.is_cuda:
+            from .fused import head_bce_loss, head_supported
+
+            if head_supported(x, self.linear.weight, labels):
+                return head_bce_loss(x, self.linear.weight, self.linear.bias, labels, self.dropout.p,
+                                     self.training)
+        out = self.linear(self.dropout(F.normalize(x, p=2, dim=1)))
+        return loss(out, labels, sigmoid_loss, x.device), out
+
 
 def loss(preds, labels, sigmoid_loss, device):
     """utils.py:129-140: BCE-with-logits (or CE) weighted by 1/batch, summed."""

@@ -76,8 +76,11 @@ class Trainer:
         for p in self.params:
             p.grad = None
         self.model.train()
-        out = self.model(x0, adjs, sampled_nodes)
-        loss = loss_fn(out, labels, self.sigmoid_loss, self.device)
+        if hasattr(self.model, "forward_loss"):
+            loss, _ = self.model.forward_loss(x0, adjs, sampled_nodes, labels, self.sigmoid_loss)
+        else:
+            out = self.model(x0, adjs, sampled_nodes)
+            loss = loss_fn(out, labels, self.sigmoid_loss, self.device)
         loss.backward()
         if self.native:
             if self.world > 1:

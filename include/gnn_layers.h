@@ -59,6 +59,28 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
                  int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
                  size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Classifier head + loss (head.hip). Replaces GNN.forward's tail (models.py:90-97:
+ * F.normalize(x, 2, 1) -> dropout(p) -> nn.Linear(D, C)) and utils.loss with sigmoid_loss
+ * (utils.py:129-140: BCEWithLogitsLoss(weight = 1/M per row, reduction "sum")):
+ *   xd = dropout(x / max(||x||, 1e-12))  -> stored M x D (row stride D) for dW = dzᵀ·xd
+ *   z  = xd·Wᵀ + bias                    -> stored M x C (logits)
+ *   *loss = Σ_rows Σ_j (max(z,0) - z y + log1p(exp(-|z|))) / M   (rows summed in fixed order)
+ * norm[M] = ||x|| per row, rowloss[M] = the per-row terms (workspace). W is C x D row-major
+ * (nn.Linear.weight), labels M x C with row stride ldl; bias may be NULL. D % 4 == 0,
+ * D <= 2048, C <= 64; X, W, xd 16-byte aligned. Dropout: the counter hash of (seed, r*D+c)
+ * (as gnn_sage_norm_*), training = 0 or p = 0 disables it.
+ * Backward: dz = (*grad_loss) (sigmoid(z) - y) / M (M x C, written for dW / db), and
+ * dX = d/dx of the normalisation applied to mask · (dz·W). grad_loss may be NULL (1).
+ * ------------------------------------------------------------------------------- */
+int gnn_head_bce_fwd_f32(const float* X, int64_t ldx, int64_t M, int64_t D, const float* W, const float* bias,
+                         int64_t C, const float* labels, int64_t ldl, float p, uint64_t seed, int training,
+                         float* xd, float* z, float* norm, float* rowloss, float* loss, void* stream);
+int gnn_head_bce_bwd_f32(const float* X, int64_t ldx, int64_t M, int64_t D, const float* W, int64_t C,
+                         const float* labels, int64_t ldl, const float* grad_loss, float p, uint64_t seed,
+                         int training, const float* z, const float* norm, float* dz, float* dX, int64_t lddx,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

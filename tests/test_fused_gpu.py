@@ -137,3 +137,100 @@ def test_gpu_model_step_matches_reference(dev, golden, name, fused):
         sure = np.abs(g) > 1e-5 * max(np.abs(g).max(), 1e-12)
         got = prm.detach().cpu().numpy()
         np.testing.assert_allclose(got[sure], st[f"{name}_step_{pname}"][sure], rtol=1e-4, atol=1e-5, err_msg=pname)
+
+
+def _head_ref(x, W, b, y, mask=None, p=0.0):
+    """GNN's tail (models.py:90-97) + utils.loss (utils.py:129-140) in torch; `mask` replaces
+    the dropout draw (1 kept / 0 dropped)."""
+    h = F.normalize(x, p=2, dim=1)
+    if mask is not None:
+        h = h * mask / (1 - p)
+    z = F.linear(h, W, b)
+    return loss(z, y, True, x.device), z
+
+
+@pytest.mark.parametrize("M,D,C", [(512, 1024, 41), (37, 512, 41), (1, 64, 3), (100, 2048, 64), (5, 4, 1)])
+def test_head_bce_matches_torch(dev, M, D, C):
+    """Fused head + BCE (gnn_head_bce_*), eval mode, against an fp64 torch evaluation:
+    rtol 1e-4 / atol 1e-5 (row reductions of up to 2048 terms in another order)."""
+    from gnn_amd.fused import head_bce_loss
+
+    g = torch.Generator().manual_seed(M * 7 + D + C)
+    x = torch.randn(M, D, generator=g)
+    x[0] *= 1e-3
+    if M > 3:
+        x[3] = 0.0  # a zero row: the norm is clamped to 1e-12
+    W = torch.randn(C, D, generator=g) * 0.1
+    b = torch.randn(C, generator=g)
+    y = (torch.rand(M, C, generator=g) < 0.3).float()
+    leaves64 = [t.double().requires_grad_(True) for t in (x, W, b)]
+    l64, z64 = _head_ref(*leaves64, y.double())
+    l64.backward()
+    leaves = [t.to(dev).requires_grad_(True) for t in (x, W, b)]
+    lo, z = head_bce_loss(*leaves, y.to(dev), p=0.1, training=False)
+    lo.backward()
+    np.testing.assert_allclose(z.cpu().numpy(), z64.detach().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(float(lo), float(l64), rtol=1e-5)
+    for a, r in zip(leaves[1:], leaves64[1:]):
+        np.testing.assert_allclose(a.grad.cpu().numpy(), r.grad.numpy(), rtol=1e-4, atol=1e-5)
+    # d(x) = (d(xn) - xn (xn · d(xn))) / ||x||: the projection cancels, so the error scales
+    # with the row's gradient magnitude — tolerance per row
+    got, ref = leaves[0].grad.cpu().double().numpy(), leaves64[0].grad.numpy()
+    rowmax = np.abs(ref).max(axis=1, keepdims=True)
+    assert np.all(np.abs(got - ref) <= 1e-4 * np.abs(ref) + 1e-5 * np.maximum(rowmax, 1.0))
+
+
+def test_head_bce_dropout(dev):
+    """Training mode: the mask the forward drew (read back from the stored dropout output)
+    reproduces the loss, and the backward regenerates the same mask."""
+    from gnn_amd import _lib
+
+    M, D, C, p = 512, 1024, 41, 0.1
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, D, generator=g).to(dev)
+    W = (torch.randn(C, D, generator=g) * 0.1).to(dev)
+    b = torch.randn(C, generator=g).to(dev)
+    y = (torch.rand(M, C, generator=g) < 0.3).float().to(dev)
+    xd = torch.empty(M, D, device=dev)
+    z = torch.empty(M, C, device=dev)
+    nrm = torch.empty(M, device=dev)
+    rl = torch.empty(M, device=dev)
+    lo = torch.empty((), device=dev)
+    st = _lib.stream_of(dev)
+    L = _lib.lib()
+    _lib.check(L.gnn_head_bce_fwd_f32(x.data_ptr(), D, M, D, W.data_ptr(), b.data_ptr(), C, y.data_ptr(), C, p, 1234,
+                                      1, xd.data_ptr(), z.data_ptr(), nrm.data_ptr(), rl.data_ptr(), lo.data_ptr(),
+                                      st), "fwd")
+    gl = torch.full((), 2.0, device=dev)
+    dz = torch.empty(M, C, device=dev)
+    dx = torch.empty(M, D, device=dev)
+    _lib.check(L.gnn_head_bce_bwd_f32(x.data_ptr(), D, M, D, W.data_ptr(), C, y.data_ptr(), C, gl.data_ptr(), p, 1234,
+                                      1, z.data_ptr(), nrm.data_ptr(), dz.data_ptr(), dx.data_ptr(), D, st), "bwd")
+    torch.cuda.synchronize()
+    mask = (xd != 0).float()
+    assert abs(mask.mean().item() - (1 - p)) < 0.005
+    xr = x.clone().requires_grad_(True)
+    lr, zr = _head_ref(xr, W, b, y, mask, p)
+    (2.0 * lr).backward()
+    torch.testing.assert_close(xd, F.normalize(x, dim=1) * mask / (1 - p), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(z, zr, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(lo, lr.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["graphsage", "gcn"])
+def test_gpu_forward_loss_matches_reference(dev, golden, name):
+    """GNN.forward_loss (fused encoder + fused head/BCE) reproduces the reference's seeded
+    CPU step: loss, logits and every parameter gradient (eval mode)."""
+    st = golden("model_step_tiny.npz")
+    adjs, sampled, x0, y = _golden_inputs(golden, dev)
+    torch.manual_seed(0)
+    net = build_model(name, 602, 32, [1, 1, 1], 41, dropout=0.1, fused=True).to(dev)
+    net.eval()
+    lo, out = net.forward_loss(x0, adjs, sampled, y, True)
+    lo.backward()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), st[f"{name}_out"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(float(lo), float(st[f"{name}_loss"]), rtol=1e-5)
+    for pname, prm in net.named_parameters():
+        np.testing.assert_allclose(prm.grad.cpu().numpy(), st[f"{name}_grad_{pname}"], rtol=2e-3, atol=1e-5,
+                                   err_msg=pname)
