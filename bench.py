@@ -225,7 +225,7 @@ def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):
 
     def nxt():
         lb = next(it)
-        return lb.plan, lb.host.to_device(dev, build=False)
+        return lb.plan, lambda: lb.host.to_device(dev, with_coo=False)
 
     warm = max(2 * workers, 10)
     pipeline(nxt, warm)
@@ -297,7 +297,7 @@ def main():
     stager = staging.Stager(store, exchange)
     plans = [staging.make_plan(hb, store, rank, world) for hb in host_batches]
     # CSR pieces, labels and sampled_nodes resident in HBM; the operand builder (the
-    # create_coo_tensor kernel) and the backward's transpose run inside every step.
+    # create_coo_tensor kernel) runs for every step, on the staging stream ahead of it.
     dbatches = [hb.to_device(dev, build=False) for hb in host_batches]
     if args.dump_batch and rank == 0:
         L0 = host_batches[0].layers
@@ -314,19 +314,17 @@ def main():
     nb = len(dbatches)
 
     def pipeline(next_item, steps):
-        """next_item() -> (StagePlan, DeviceBatch). X0 staging of batch i+1 is issued on the
-        side stream before batch i's step, so its copies overlap that step's kernels."""
+        """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
+        needed + the operand builds). Batch i+1's X0 staging and batch_fn run on the side
+        stream, issued before batch i's step, so they overlap that step's kernels."""
         loss = None
-        cur = next_item()
-        staged = stager.issue(cur[0])
+        staged = stager.issue(*next_item())
         for i in range(steps):
-            nxt = next_item() if i + 1 < steps else None
-            staged_next = stager.issue(nxt[0]) if nxt is not None else None
+            staged_next = stager.issue(*next_item()) if i + 1 < steps else None
             x0 = staged.wait()
-            db = cur[1]
-            adjs = db.build_operands()
-            loss = trainer.step(x0, adjs, db.sampled_nodes, db.labels)
-            cur, staged = nxt, staged_next
+            db = staged.batch
+            loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
+            staged = staged_next
         return loss
 
     def run(steps, start):
@@ -336,7 +334,8 @@ def main():
         def nxt():
             j = k[0] % nb
             k[0] += 1
-            return plans[j], dbatches[j]
+            db = dbatches[j]
+            return plans[j], lambda: (db.build_operands(), db)[1]
         return pipeline(nxt, steps)
 
     run(args.warmup, 0)

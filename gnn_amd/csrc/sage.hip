@@ -15,6 +15,7 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 
 #include "common.h"
 #include "gnn_layers.h"
@@ -25,7 +26,18 @@ using gnn::ceil_div;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int SN_MAXV = 8;   // float4 per lane: D <= 64 * 4 * 8 = 2048
-constexpr int BWD_MAX_GRID = 512;
+constexpr int BWD_MAX_GRID = 768;  // 3 workgroups per CU (158 VGPRs at D = 1024): rows overlap their latencies
+
+// backward grid cap (env GNN_SAGE_BWD_GRID overrides, for sweeps; the workspace is sized by
+// the larger of the two)
+int bwd_grid_cap() {
+  static const int cap = [] {
+    const char* e = std::getenv("GNN_SAGE_BWD_GRID");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 && v <= 4096 ? v : BWD_MAX_GRID;
+  }();
+  return cap;
+}
 constexpr int NRED = 3;      // column sums: d(scale), d(offset), d(bias)
 
 __device__ __forceinline__ float wave_sum(float x) {
@@ -323,7 +335,8 @@ int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float*
 }
 
 size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
-  const int64_t G = M <= 0 ? 1 : (ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID);
+  const int64_t cap = bwd_grid_cap();
+  const int64_t G = M <= 0 ? 1 : (ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap);
   return gnn::align_up((size_t)G * NRED * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
 }
 
@@ -352,7 +365,8 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
   GNN_REQUIRE(workspace && workspace_bytes >= gnn_sage_norm_bwd_workspace_bytes(M, D),
               "gnn_sage_norm_bwd_f32: workspace too small");
   const int nv = (int)ceil_div(D, 256);
-  const int64_t G = ceil_div(M, 4) < BWD_MAX_GRID ? ceil_div(M, 4) : BWD_MAX_GRID;
+  const int64_t cap = bwd_grid_cap();
+  const int64_t G = ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap;
   const float inv_keep = 1.0f / (1.0f - p_drop);
   float* partial = (float*)workspace;
   hipLaunchKernelGGL(bwd_fn(nv), dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st, gY, ldg,

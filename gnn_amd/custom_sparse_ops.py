@@ -101,6 +101,14 @@ class CsrOperand:
     def device(self) -> torch.device:
         return self.val.device
 
+    def tensors(self) -> tuple:
+        """The device tensors of the operand and of its cached transpose (for record_stream
+        when the operand is built on another stream than the one that reads it)."""
+        ts = (self.rowptr, self.col, self.val)
+        if self._t is not None:
+            ts += (self._t.rowptr, self._t.col, self._t.val)
+        return ts
+
     def transpose(self) -> "CsrOperand":
         if self._t is None:
             M, K = self.shape

@@ -114,6 +114,20 @@ class DeviceBatch:
     sampled_nodes: list
     labels: torch.Tensor
 
+    def tensors(self) -> list:
+        """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
+        maps), labels and the built operands (record_stream across streams)."""
+        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6]) if t is not None]
+        for x in self.sampled_nodes:
+            ts.append(x)
+            if getattr(x, "_gnn_rmap", None) is not None:
+                ts.append(x._gnn_rmap)
+        ts.append(self.labels)
+        for a in self.adjs or []:
+            if a is not None:
+                ts.extend(a.tensors() if hasattr(a, "tensors") else a._gnn_csr.tensors())
+        return ts
+
     def build_operands(self, with_coo: bool = False) -> list:
         """create_coo_tensor for every layer (stream-ordered on the current stream)."""
         from . import custom_sparse_ops as cso

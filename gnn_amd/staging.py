@@ -120,7 +120,11 @@ class Stager:
         recs[-1][1].synchronize()
         return sum(b for _, _, b in recs), sum(a.elapsed_time(b) for a, b, _ in recs) * 1e-3
 
-    def issue(self, plan: StagePlan):
+    def issue(self, plan: StagePlan, batch_fn=None):
+        """Issue X0's assembly (and, with ``batch_fn``, the batch's device side: batch_fn() runs
+        on the staging stream and returns the DeviceBatch — its H2D copies and operand
+        builds then overlap the previous step too). ``wait()`` on the result orders the
+        compute stream after all of it."""
         dev = self.device
         st = self.stream
         if self.exchange is not None:
@@ -143,18 +147,24 @@ class Stager:
             extra = ()
             if self.exchange is not None:
                 extra = self.exchange.exchange(plan, x0, self.store)
+            batch = batch_fn() if batch_fn is not None else None
             ev = torch.cuda.Event()
             ev.record(st)
         keep = (own_pos, own_src, host_pos, host_dev) + tuple(extra)
-        return StagedX0(x0, ev, keep, self.store.F)
+        if batch is not None:
+            keep += tuple(batch.tensors())
+        return StagedX0(x0, ev, keep, self.store.F, batch)
 
 
 class StagedX0:
-    def __init__(self, x0, event, keep, F):
+    def __init__(self, x0, event, keep, F, batch=None):
         self._x0 = x0
         self.event = event
         self._keep = keep
         self.F = F
+        self.batch = batch  # the DeviceBatch built on the staging stream, if any
+        # its operands as built by this issue (a later issue may rebuild the same batch)
+        self.adjs = list(batch.adjs) if batch is not None and batch.adjs is not None else None
 
     def wait(self) -> torch.Tensor:
         """Make the current stream wait for the staging and return the (n x F) view."""

@@ -1,0 +1,61 @@
+"""GPU: batch staging on the side stream — X0 assembly plus the batch's H2D copies and
+operand builds (Stager.issue(plan, batch_fn)) — gives the compute stream exactly the inputs
+a build on the compute stream gives: X0 rows bit-identical to the feature table, operands
+bit-identical, and the same training-step loss."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from gnn_amd import loader, placement, staging
+from gnn_amd.graphs import chung_lu, row_normalize
+from gnn_amd.models import build_model
+from gnn_amd.train import Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(N=6000, avg=16, seed=5):
+    A = chung_lu(N, N * avg // 2, 1.3, np.random.default_rng(seed))
+    lap = row_normalize(A)
+    lap.sum_duplicates()
+    labels = sp.csr_matrix((np.ones(N, np.float32), (np.arange(N), np.arange(N) % 7)), shape=(N, 7))
+    train = np.arange(0, N, 2)
+    return lap, labels, train
+
+
+def test_side_stream_batch_matches_compute_stream(dev):
+    lap, labels, train = _setup()
+    N = lap.shape[0]
+    pl = placement.create_buffer_ours(lap, train, 500, [0], 3, alpha=0)
+    feats = torch.randn(N, 30)
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    ld = loader.BatchLoader(lap, labels, train, 800, 128, [1, 1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], rank=0, world_size=1, store=store, workers=2,
+                            seed=21)
+    lbs = list(ld.epoch(1))[:3]
+    ld.close()
+    stager = staging.Stager(store)
+    torch.manual_seed(0)
+    m1 = build_model("graphsage", 30, 16, [1, 1, 1], 7, dropout=0.0, fused=True).to(dev)
+    torch.manual_seed(0)
+    m2 = build_model("graphsage", 30, 16, [1, 1, 1], 7, dropout=0.0, fused=True).to(dev)
+    t1, t2 = Trainer(m1, 0.01, dev), Trainer(m2, 0.01, dev)
+    for lb in lbs:
+        # side stream: X0 + H2D + operand builds, issued before anything else touches them
+        staged = stager.issue(lb.plan, lambda: lb.host.to_device(dev, with_coo=False))
+        x0 = staged.wait()
+        db = staged.batch
+        # reference: everything on the compute stream
+        ref = lb.host.to_device(dev, with_coo=False)
+        assert torch.equal(x0.cpu(), feats[torch.from_numpy(lb.host.input_nodes)])
+        for a, b in zip(staged.adjs, ref.adjs):
+            assert torch.equal(a.rowptr, b.rowptr) and torch.equal(a.col, b.col) and torch.equal(a.val, b.val)
+            ta, tb = a.transpose(), b.transpose()
+            assert torch.equal(ta.rowptr, tb.rowptr) and torch.equal(ta.col, tb.col) and torch.equal(ta.val, tb.val)
+        l1 = t1.step(x0, staged.adjs, db.sampled_nodes, db.labels)
+        x0r = x0.clone()
+        l2 = t2.step(x0r, ref.adjs, ref.sampled_nodes, ref.labels)
+        assert float(l1) == float(l2)
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(p1, p2)
