@@ -349,6 +349,7 @@ class HeadBCEFn(torch.autograd.Function):
         ctx.save_for_backward(x, W, labels, xd, z, nrm)
         ctx.cfg = (float(p), int(training), int(seed), b is not None)
         ctx.mark_non_differentiable(z)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the logits output
         return loss, z
 
     @staticmethod

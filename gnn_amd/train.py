@@ -81,7 +81,14 @@ class Trainer:
         else:
             out = self.model(x0, adjs, sampled_nodes)
             loss = loss_fn(out, labels, self.sigmoid_loss, self.device)
-        loss.backward()
+        if self.native:
+            # d(loss)/d(loss) = 1 from a cached device scalar (no fill launch per step)
+            one = getattr(self, "_one", None)
+            if one is None or one.device != loss.device:
+                one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+            loss.backward(one)
+        else:
+            loss.backward()
         if self.native:
             if self.world > 1:
                 flat = self.optimizer.clip_to_flat()  # this rank's clip, into the all-reduce buffer
