@@ -934,16 +934,21 @@ int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
 }
 
 int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
-  (void)M;
   (void)F;
   // Units are equal-sized (S nonzeros), which balances power-law rows by construction.
   // Measured on the Reddit LADIES layers (scripts/spmm_microbench.py, with L2 column
   // tiles): S = 256 is the sweet spot between per-row flush/search overhead (small S) and
   // too few waves per column-tile pass (large S: layer-1 forward 262 us at S = 404 vs
-  // 208 us at 256). Small problems keep >= 2048 units for parallelism, S >= 16.
+  // 208 us at 256). Small problems keep >= 2048 units for parallelism, S >= 16. Operands
+  // with < 16 nonzeros per row on average are mostly output rows to write (the layer-2
+  // backward: 8.7 k rows, 1.7 nonzeros each): about two rows per unit, S >= 4 (18 vs 23 us).
   int64_t s = 256;
   if (ceil_div(nnz, s) < 2048) s = ceil_div(nnz, 2048);
   if (s < 16) s = 16;
+  if (M > 0 && nnz < 16 * M) {
+    const int64_t r = 2 * nnz / M;
+    s = std::min<int64_t>(s, r < 4 ? 4 : r);
+  }
   return s;
 }
 

@@ -76,6 +76,9 @@ def test_workspace_and_config():
 
     L = _lib.lib()
     assert L.gnn_spmm_default_unit_nnz(15809, 1810000, 602) >= 16
+    # very sparse rows (the layer-2 backward operand): ~2 rows per unit, never below 4
+    assert L.gnn_spmm_default_unit_nnz(8680, 14876, 1024) == 4
+    assert L.gnn_spmm_default_unit_nnz(1000, 100, 64) == 4
     ws = L.gnn_spmm_workspace_bytes(15809, 1810000, 602, 0)
     unit = L.gnn_spmm_default_unit_nnz(15809, 1810000, 602)
     assert ws >= ((1810000 + unit - 1) // unit) * 2 * 604 * 4
