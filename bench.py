@@ -206,9 +206,24 @@ def cpu_baseline(args, hb, feats, num_classes):
             "spmm_call_ms": calls}
 
 
+def cpu_budget() -> int:
+    """Host CPUs this process may use: the affinity set, capped by a cgroup-v2 CPU quota
+    (the GPU box grants 16 CPUs per GPU by quota while os.cpu_count() shows the machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def default_workers(world: int) -> int:
-    # the GPU box grants ~16 host CPUs per GPU (os.cpu_count() shows the whole machine)
-    return max(2, min(10, (os.cpu_count() or 8) // max(world, 1) - 4))
+    # sampler threads per rank: the rank's CPU share minus the training thread and one spare
+    # (measured on the 16-CPU box: 14 threads 288 mini-batches/s end to end, 10 threads 227)
+    return max(2, min(14, cpu_budget() // max(world, 1) - 2))
 
 
 def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):

@@ -157,14 +157,35 @@ class Work {
   // Column nonzero counts of U = lap[rows, :] (sp.linalg.norm(U, ord=0, axis=0)); `live` =
   // ascending columns with a non-zero count (one sequential scan, no sort); returns the sum.
   int64_t count_columns(const std::vector<int64_t>& rows) {
+    for (int64_t v : rows) add_row(v);
+    return scan_counts();
+  }
+
+  // Same counts when rows ⊇ the rows already counted (LADIES: each layer's rows are the
+  // previous layer's rows plus the newly sampled ones, sampler.py:131) — only the rows not
+  // counted yet are added; the counts are kept across layers (the layer-2 U has 5.7 M
+  // entries of which 3.5 M are the layer-1 rows').
+  int64_t count_columns_nested(const std::vector<int64_t>& rows) {
+    if (counted.empty()) counted.assign(g_.N, 0);
     for (int64_t v : rows) {
-      const int64_t b = g_.indptr[v], e = g_.indptr[v + 1];
-      if (g_.data) {
-        for (int64_t k = b; k < e; ++k) cnt[(size_t)g_.indices[k]] += (g_.data[k] != 0.0f);
-      } else {
-        for (int64_t k = b; k < e; ++k) ++cnt[(size_t)g_.indices[k]];
+      if (!counted[(size_t)v]) {
+        counted[(size_t)v] = 1;
+        add_row(v);
       }
     }
+    return scan_counts();
+  }
+
+  void add_row(int64_t v) {
+    const int64_t b = g_.indptr[v], e = g_.indptr[v + 1];
+    if (g_.data) {
+      for (int64_t k = b; k < e; ++k) cnt[(size_t)g_.indices[k]] += (g_.data[k] != 0.0f);
+    } else {
+      for (int64_t k = b; k < e; ++k) ++cnt[(size_t)g_.indices[k]];
+    }
+  }
+
+  int64_t scan_counts() {
     int64_t isum = 0;
     live.clear();
     for (size_t c = 0; c < g_.N; ++c) {
@@ -263,7 +284,7 @@ class Work {
   std::vector<int32_t> cnt;  // column nonzero counts of U (< nnz < 2^31)
   std::vector<uint64_t> bits;
   std::vector<int32_t> wrank;
-  std::vector<uint8_t> taken, in_prev;
+  std::vector<uint8_t> taken, in_prev, counted;
   std::vector<int64_t> live, found;
 };
 
@@ -312,13 +333,22 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
     res->layers.resize((size_t)num_layers);
     MT19937 rng(seed);
     std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size), after;
+    // A batch with repeated nodes repeats rows of U (counted twice); later layers' rows are
+    // unique. Counts carry over between layers only when every layer's rows are unique.
+    bool nested = true;
+    for (int64_t v : prev) {
+      if (w.in_prev[(size_t)v]) nested = false;
+      w.in_prev[(size_t)v] = 1;
+    }
+    for (int64_t v : prev) w.in_prev[(size_t)v] = 0;
     for (int32_t d = 0; d < num_layers; ++d) {
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
       if (orders[num_layers - 1 - d] == 0) continue;         // orders1 = orders[::-1]
       L.present = true;
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
       if (unnz < 0) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
-      const int64_t isum = w.count_columns(prev);  // p = pi / sum(pi): exact integer sum
+      // p = pi / sum(pi): exact integer sum
+      const int64_t isum = nested ? w.count_columns_nested(prev) : w.count_columns(prev);
       if (isum == 0)  // p = 0/0: numpy's choice raises "probabilities contain NaN"
         return fail("gnn_ladies_sample: probabilities contain NaN (layer %d: no entries in U)", d);
       const double total = (double)isum;
@@ -331,8 +361,12 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
       w.positions(after, prev, L);
       L.M = (int64_t)prev.size();
       L.K = (int64_t)after.size();
-      w.clear_counts();
-      prev.swap(after);
+      if (!nested) {
+        w.clear_counts();
+        nested = true;  // after = unique(...): from here on every layer's rows are unique
+        w.counted.clear();
+      }
+      prev.swap(after);  // after ⊇ prev: the next layer's counts extend these
     }
     res->input_nodes = prev;
     *out = res.release();

@@ -101,6 +101,17 @@ def test_native_exhausts_support():
     _same(a, b)
 
 
+@pytest.mark.parametrize("orders", [[1, 1, 1], [1, 1, 0], [1, 0, 1]])
+def test_native_repeated_batch_nodes(orders):
+    """A batch with repeated nodes repeats rows of U (their columns counted twice), so the
+    column counts cannot carry over into the next layer there; later layers' rows are unique."""
+    N = 4000
+    lap = _lap(N, 12, 4)
+    batch = np.concatenate([np.arange(200, 260), np.arange(230, 250), [777, 777]])
+    a, b = _both(lap, N, batch, [600, 400, 300], orders, 13)
+    _same(a, b)
+
+
 def test_native_orders_with_zero_layers():
     N = 2000
     lap = _lap(N, 10, 8)
