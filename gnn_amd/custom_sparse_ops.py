@@ -189,7 +189,7 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
     F = dense.shape[1]
     ldx = dense.stride(0) if dense.shape[0] > 1 else max(F, 1)
     dev = dense.device
-    # Padded rows (the layer-0 staging buffer: 602 floats in 604-float rows): let the
+    # Padded rows (the layer-0 staging buffer: 602 floats in 608-float rows): let the
     # kernel run over the padded width Fk = round_up(F, 4) so it can use 16-byte loads, into
     # an output with the same padded stride; the caller gets the (M x F) view.
     if rmap is not None:
@@ -205,8 +205,11 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
         avail = dense.untyped_storage().nbytes() // 4 - dense.storage_offset()
         if ldx >= F4 and (K - 1) * ldx + F4 <= avail:
             Fk = F4
+    # A padded input gets an output with the same row stride (line-aligned rows for the
+    # consumer GEMM and whole-line row stores).
+    ldo = ldx if (Fk != F and ldx <= 2 * Fk) else Fk
     with _lib.on_device(dev):
-        out = torch.empty((M, Fk), dtype=torch.float32, device=dev)
+        out = torch.empty((M, ldo), dtype=torch.float32, device=dev)
         if M == 0 or F == 0:
             return out[:, :F]
         L = _lib.lib()
@@ -220,7 +223,7 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
             e1.record()
             L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
             cfg = (ctypes.c_int32 * 6)()
-            L.gnn_spmm_config(M, K, op.nnz, Fk, ldx, Fk, dense.data_ptr(), out.data_ptr(), unit_nnz, cfg)
+            L.gnn_spmm_config(M, K, op.nnz, Fk, ldx, ldo, dense.data_ptr(), out.data_ptr(), unit_nnz, cfg)
             u = 4 if cfg[2] <= 4 else (3 if cfg[2] == 5 else 2)  # pick_u (spmm.hip)
             nbytes = algorithmic_bytes(M, op.nnz, F)
             if rmap is not None:  # residual rows read + the row map
@@ -230,12 +233,12 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
                                     f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>"))
         if rmap is None:
             _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
-                                          dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
+                                          dense.data_ptr(), ldx, out.data_ptr(), ldo, Fk,
                                           ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32")
         else:
             ldr = residual.stride(0) if residual.shape[0] > 1 else max(F, 1)
             _lib.check(L.gnn_spmm_csr_f32_ex(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
-                                             dense.data_ptr(), ldx, out.data_ptr(), Fk, Fk,
+                                             dense.data_ptr(), ldx, out.data_ptr(), ldo, Fk,
                                              residual.data_ptr(), ldr, rmap.data_ptr(),
                                              ws.data_ptr(), wsb, unit_nnz, st), "gnn_spmm_csr_f32_ex")
     return out if Fk == F else out[:, :F]

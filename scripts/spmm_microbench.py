@@ -41,20 +41,23 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--units", default="0,16,32,64,128,256,512")
     ap.add_argument("--out", default="")
+    ap.add_argument("--f0", default="602,600", help="layer-0 widths; F:ld reads an F-wide view of ld-wide rows")
+    ap.add_argument("--layers", default="0,1,2")
     args = ap.parse_args()
     z = np.load(args.batch)
     dev = torch.device("cuda", 0)
     res = []
-    for li in range(3):
+    for li in [int(v) for v in args.layers.split(",")]:
         shape = tuple(int(v) for v in z[f"l{li}_shape"])
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         op, _ = cso.build_operand(t(z[f"l{li}_fullrowptr"]), t(z[f"l{li}_rowptr"]), t(z[f"l{li}_colidx"]),
                                   t(z[f"l{li}_normfact"]), shape[0], shape[1], with_coo=False)
-        Fs = [602, 600] if li == 0 else [1024]
+        Fs = args.f0.split(",") if li == 0 else ["1024"]
         sites = [("fwd", op)] if li == 0 else [("fwd", op), ("bwd", op.transpose())]
         for tag, o in sites:
-            for F in Fs:
-                X = torch.randn(o.shape[1], F, device=dev)
+            for fs in Fs:
+                F, ld = (int(v) for v in fs.split(":")) if ":" in fs else (int(fs), int(fs))
+                X = torch.randn(o.shape[1], ld, device=dev)[:, :F]
                 for unit in [int(u) for u in args.units.split(",")]:
                     cso.spmm_csr(o, X, unit_nnz=unit)  # warm
                     ms, nbytes, tms = time_call(o, X, unit, args.reps)
@@ -63,6 +66,7 @@ def main():
                                units=cfg["units"], vw=cfg["vw"], g=cfg["g"], nj=cfg["nj"], us=round(ms * 1e3, 1),
                                GBps=round(nbytes / (ms * 1e-3) / 1e9, 1), call_us=round(tms * 1e3, 1),
                                call_GBps=round(nbytes / (tms * 1e-3) / 1e9, 1))
+                    row["ld"] = ld
                     res.append(row)
                     print(json.dumps(row), flush=True)
         # operand build + transpose costs
