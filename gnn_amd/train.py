@@ -111,9 +111,13 @@ def init_distributed(backend: Optional[str] = None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not torch.distributed.is_initialized():
-        be = backend or ("nccl" if torch.cuda.is_available() else "gloo")
-        if be == "nccl":
+        be = backend or os.environ.get("GNN_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            # one GPU per local rank (torchrun); more ranks than GPUs (a rehearsal on a smaller
+            # box, gloo backend: RCCL refuses two ranks on one GPU) share them round-robin
+            local = local % max(torch.cuda.device_count(), 1)
             torch.cuda.set_device(local)
+        if be == "nccl":
             torch.distributed.init_process_group(be, device_id=torch.device("cuda", local))
         else:
             torch.distributed.init_process_group(be)
