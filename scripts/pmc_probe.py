@@ -6,7 +6,7 @@
    with the SAME row width / vector width as the aggregation kernel being measured, so the
    read bytes are known exactly.
 2. The forward aggregations of the benchmark's batch 0, R times each, with the operands laid
-   out as bench.py runs them (layer 0: X0 in 604-float padded rows; layers 1-2: 1024 wide),
+   out as bench.py runs them (layer 0: X0 in padded rows, staging.padded_ld — 608 floats for 602; layers 1-2: 1024 wide),
    so the kernel instantiations — the names rocprofv3 reports — are the benchmark's.
 """
 import argparse
@@ -18,6 +18,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gnn_amd import custom_sparse_ops as cso  # noqa: E402
+from gnn_amd.staging import padded_ld  # noqa: E402
 
 
 def main():
@@ -29,7 +30,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     F = args.feat
-    ld = (F + 3) // 4 * 4
+    ld = padded_ld(F)
     # calibration table: rows of ld floats (16-byte vectors, as the aggregation's X0 reads)
     n = int(1.2e9 // (ld * 4))
     g = torch.Generator(device=dev).manual_seed(0)
