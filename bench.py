@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=60, help="steps of the live-sampling end-to-end run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the live-sampling end-to-end run")
     ap.add_argument("--workers", type=int, default=0, help="sampler threads per rank (0: auto)")
+    ap.add_argument("--staging", default="copy", choices=["copy", "zerocopy"],
+                    help="non-buffered feature rows: host gather into pinned memory + one hipMemcpyAsync "
+                         "(copy), or the GPU reads the mapped host table over PCIe (zerocopy: measured "
+                         "slower, it slows the concurrent compute kernels)")
     ap.add_argument("--cprofile", default="", help="after the timed run, cProfile 20 steps into this text file")
     ap.add_argument("--torch-profile", default="", help="after the timed run, write a torch.profiler op table here")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
@@ -307,7 +311,7 @@ def main():
         log(f"pmc traffic done ({time.time() - t0:.1f}s): {traffic}")
     torch.cuda.set_device(dev)
 
-    store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank)
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank, zero_copy=args.staging == "zerocopy")
     exchange = staging.PeerExchange() if world > 1 else None
     stager = staging.Stager(store, exchange)
     plans = [staging.make_plan(hb, store, rank, world) for hb in host_batches]
@@ -373,10 +377,13 @@ def main():
         elapsed = float(t.item())
     recs = cso.take_timing_records()
     h_bytes, h_sec = stager.take_timing()
-    staging_info = {"host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
+    staging_info = {"mode": args.staging, "host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
                     "h2d_GBps": round(h_bytes / h_sec / 1e9, 1) if h_sec > 0 else None,
                     "h2d_ms_per_batch": round(1e3 * h_sec / args.steps, 3),
-                    "note": "pinned host rows -> HBM on the staging stream, overlapped with the previous step"}
+                    "note": ("GPU gather of the host rows from the pinned, device-mapped feature table over PCIe"
+                             if args.staging == "zerocopy" else
+                             "host rows gathered into pinned memory by the producer, one hipMemcpyAsync")
+                            + " on the staging stream, overlapped with the previous step"}
 
     # ------------------------------------------------- end to end, live sampling
     e2e = None

@@ -27,6 +27,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <atomic>
 #include <mutex>
@@ -918,6 +919,55 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
+// Rows read straight from pinned, device-mapped host memory (zero-copy over PCIe): a small
+// persistent grid (each wave two rows per pass, every load of both rows issued before the
+// first store) keeps a few MB of PCIe reads in flight while holding few CU slots, so the
+// gather runs on the staging stream beside the compute kernels.
+// Measured on MI355X (Reddit batch, 31 MB of host rows): 46-51 GB/s at 32-128 workgroups,
+// 24 GB/s at 8 — but the PCIe reads slow the concurrent compute kernels (GPU step 2.18 ->
+// 2.50-2.64 ms at every grid tried), so bench.py defaults to the pinned-copy path.
+constexpr int HOST_GATHER_GRID = 32;
+
+template <int VW>
+__global__ __launch_bounds__(256) void gather_rows_host_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                               const int64_t* __restrict__ src_idx,
+                                                               float* __restrict__ dst, int64_t ld_dst,
+                                                               const int64_t* __restrict__ dst_idx, int64_t n, int F) {
+  using V = typename Vec<VW>::T;
+  constexpr int CH = 3;  // 64 * VW-float chunks per row held in registers (608 floats at VW 4)
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t i0 = 2 * w; i0 < n; i0 += 2 * nw) {
+    V v[2][CH];
+    const float* sr[2];
+    float* dr[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t i = min(i0 + q, n - 1);  // an odd last row is simply copied twice
+      sr[q] = src + (src_idx ? src_idx[i] : i) * ld_src;
+      dr[q] = dst + (dst_idx ? dst_idx[i] : i) * ld_dst;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int c = (lane + 64 * j) * VW;
+        if (c < F) v[q][j] = *reinterpret_cast<const V*>(sr[q] + c);
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int j = 0; j < CH; ++j) {
+        const int c = (lane + 64 * j) * VW;
+        if (c < F) *reinterpret_cast<V*>(dr[q] + c) = v[q][j];
+      }
+      for (int c = (lane + 64 * CH) * VW; c < F; c += 64 * VW)  // rows wider than CH chunks
+        *reinterpret_cast<V*>(dr[q] + c) = *reinterpret_cast<const V*>(sr[q] + c);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Host-side configuration and dispatch.
 // ---------------------------------------------------------------------------------
@@ -942,7 +992,14 @@ int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
   // 208 us at 256). Small problems keep >= 2048 units for parallelism, S >= 16. Operands
   // with < 16 nonzeros per row on average are mostly output rows to write (the layer-2
   // backward: 8.7 k rows, 1.7 nonzeros each): about two rows per unit, S >= 4 (18 vs 23 us).
+  // About 2.4 rows per unit, as a power of two in [16, 256]: the layer-1 backward operand
+  // (54 nonzeros per row) 199 us at S = 128 vs 209 at 256; the forward operands (98-114 per
+  // row) keep 256.
   int64_t s = 256;
+  if (M > 0) {
+    const double want = 2.4 * (double)nnz / (double)M;
+    while (s > 16 && (double)s > want * 1.41421356) s >>= 1;
+  }
   if (ceil_div(nnz, s) < 2048) s = ceil_div(nnz, 2048);
   if (s < 16) s = 16;
   if (M > 0 && nnz < 16 * M) {
@@ -1422,6 +1479,47 @@ int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx
       break;
   }
   GNN_LAUNCHED("gather_rows_kernel");
+  return 0;
+}
+
+int gnn_host_register(void* host, size_t bytes) {
+  GNN_REQUIRE(host && bytes > 0, "gnn_host_register: NULL or empty range");
+  GNN_HIP(hipHostRegister(host, bytes, hipHostRegisterMapped), "hipHostRegister");
+  return 0;
+}
+
+int gnn_host_unregister(void* host) {
+  GNN_REQUIRE(host, "gnn_host_unregister: NULL");
+  GNN_HIP(hipHostUnregister(host), "hipHostUnregister");
+  return 0;
+}
+
+int gnn_gather_rows_host_f32(const float* host_src, int64_t ld_src, const int64_t* src_idx, float* dst,
+                             int64_t ld_dst, const int64_t* dst_idx, int64_t n, int64_t F, void* stream) {
+  GNN_REQUIRE(n >= 0 && F >= 0, "gnn_gather_rows_host_f32: negative size");
+  GNN_REQUIRE(F <= ld_src && F <= ld_dst, "gnn_gather_rows_host_f32: F exceeds a row stride");
+  GNN_REQUIRE(F < INT_MAX, "gnn_gather_rows_host_f32: F too large");
+  if (n == 0 || F == 0) return 0;
+  GNN_REQUIRE(host_src && dst, "gnn_gather_rows_host_f32: NULL src/dst");
+  void* dsrc = nullptr;
+  GNN_HIP(hipHostGetDevicePointer(&dsrc, (void*)host_src, 0),
+          "hipHostGetDevicePointer (host_src must be pinned, device-mapped host memory)");
+  const float* src = (const float*)dsrc;
+  hipStream_t st = (hipStream_t)stream;
+  const int vw = pick_vw(F, ld_src, ld_dst, src, dst);
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(n, 8), HOST_GATHER_GRID));
+  switch (vw) {
+    case 4:
+      gather_rows_host_kernel<4><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+    case 2:
+      gather_rows_host_kernel<2><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+    default:
+      gather_rows_host_kernel<1><<<grid, dim3(256), 0, st>>>(src, ld_src, src_idx, dst, ld_dst, dst_idx, n, (int)F);
+      break;
+  }
+  GNN_LAUNCHED("gather_rows_host_kernel");
   return 0;
 }
 

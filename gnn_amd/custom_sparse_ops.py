@@ -364,6 +364,30 @@ def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.T
                    "gnn_gather_rows_f32")
 
 
+def gather_rows_host(host: torch.Tensor, src_idx: torch.Tensor, dst: torch.Tensor,
+                     dst_idx: Optional[torch.Tensor], n: Optional[int] = None) -> None:
+    """dst[dst_idx] = host[src_idx], read by the GPU over PCIe from a host table registered
+    with gnn_host_register (FeatureStore(zero_copy=True)); int64 device indices."""
+    _require(not host.is_cuda and host.dtype == torch.float32 and host.stride(1) == 1,
+             "gather_rows_host: host must be a registered fp32 CPU table with contiguous rows")
+    _require(dst.is_cuda and dst.dtype == torch.float32 and dst.stride(1) == 1,
+             "gather_rows_host: dst must be a float32 CUDA tensor with contiguous rows")
+    _require(src_idx.is_cuda and src_idx.dtype == torch.int64 and src_idx.is_contiguous(),
+             "gather_rows_host: src_idx must be int64 CUDA")
+    if dst_idx is not None:
+        _require(dst_idx.is_cuda and dst_idx.dtype == torch.int64 and dst_idx.is_contiguous(),
+                 "gather_rows_host: dst_idx must be int64 CUDA")
+    F = dst.shape[1]
+    _require(host.shape[1] >= F, "gather_rows_host: source rows narrower than destination")
+    n = int(src_idx.numel()) if n is None else n
+    dev = dst.device
+    with _lib.on_device(dev):
+        _lib.check(_lib.lib().gnn_gather_rows_host_f32(host.data_ptr(), host.stride(0), src_idx.data_ptr(),
+                                                       dst.data_ptr(), dst.stride(0), _ptr(dst_idx), n, F,
+                                                       _stream(dev)),
+                   "gnn_gather_rows_host_f32")
+
+
 def spmm_config(M: int, nnz: int, F: int, ldx: Optional[int] = None, ldy: Optional[int] = None,
                 unit_nnz: int = 0, K: int = 0) -> dict:
     """Kernel configuration the library picks for a call shape (16-byte aligned buffers)."""

@@ -11,10 +11,14 @@ Here (DESIGN.md §Feature staging):
     aggregation went 386 -> 284 us on MI355X; the model sees the (n_input x F) view.
   * Own-buffer rows: one gather kernel (gnn_gather_rows_f32) from this GPU's buffer straight
     into their X0 positions.
-  * Host rows: gathered on the host into a PINNED staging tensor (by the batch producer, off
-    the critical path), then one contiguous hipMemcpyAsync on a side stream, then a scatter
-    kernel into X0 — the side stream runs ahead, overlapping the copy with the previous
-    batch's aggregation kernels; the compute stream waits on an event only when it needs X0.
+  * Host rows, zero-copy (an option; measured slower on MI355X — the PCIe reads slow the
+    concurrent compute kernels, GPU step 2.18 -> 2.5 ms): the host table lives in pinned, device-mapped
+    memory and one gather kernel on the side stream reads the batch's rows over PCIe straight
+    into their X0 positions (gnn_gather_rows_host_f32) — no host thread touches the rows.
+    Copy mode: gathered on the host into a PINNED staging tensor (by the batch producer, off
+    the critical path), then one contiguous hipMemcpyAsync on the side stream, then a scatter
+    kernel into X0. Either way the side stream runs ahead, overlapping the previous batch's
+    aggregation kernels; the compute stream waits on an event only when it needs X0.
   * Peer rows (world_size > 1): exchanged with RCCL all-to-all (``PeerExchange``): the
     request sizes and slot ids are negotiated on the host over a gloo group (no GPU sync),
     each rank gathers the rows its peers asked for from its own buffer, one
@@ -23,6 +27,7 @@ Here (DESIGN.md §Feature staging):
 from __future__ import annotations
 
 import os
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -30,6 +35,13 @@ import numpy as np
 import torch
 
 from . import custom_sparse_ops as cso
+
+
+def _host_unregister(ptr: int, device) -> None:
+    from . import _lib
+
+    with _lib.on_device(device):
+        _lib.lib().gnn_host_unregister(ptr)
 
 
 def padded_ld(F: int, align: Optional[int] = None) -> int:
@@ -41,16 +53,34 @@ def padded_ld(F: int, align: Optional[int] = None) -> int:
 
 
 class FeatureStore:
-    """Placement-resident features of one rank: its GPU buffer + the host table."""
+    """Placement-resident features of one rank: its GPU buffer + the host table.
+
+    ``zero_copy``: the host table is kept in ld-wide rows, pinned and mapped for the device
+    (gnn_host_register); the GPU then reads a batch's non-buffered rows straight from it over
+    PCIe (gnn_gather_rows_host_f32 on the staging stream) and no host thread copies rows.
+    Otherwise the batch producer gathers them into a pinned buffer for one hipMemcpyAsync."""
 
     def __init__(self, feat_data: torch.Tensor, buffer_nodes: np.ndarray, device, rank: int = 0,
-                 pin_host: bool = False):
+                 pin_host: bool = False, zero_copy: bool = False):
         assert feat_data.dtype == torch.float32 and feat_data.dim() == 2
         self.device = torch.device(device)
         self.rank = rank
         self.F = int(feat_data.shape[1])
         self.ld = padded_ld(self.F)
-        self.host = feat_data.pin_memory() if pin_host else feat_data.contiguous()
+        self.zero_copy = bool(zero_copy)
+        if self.zero_copy:
+            from . import _lib
+
+            if self.device.type != "cuda":
+                raise RuntimeError("FeatureStore(zero_copy=True) needs a CUDA device")
+            tab = torch.zeros((feat_data.shape[0], self.ld), dtype=torch.float32)
+            tab[:, : self.F] = feat_data
+            with _lib.on_device(self.device):
+                _lib.check(_lib.lib().gnn_host_register(tab.data_ptr(), tab.numel() * 4), "gnn_host_register")
+            self._unregister = weakref.finalize(self, _host_unregister, tab.data_ptr(), self.device)
+            self.host = tab
+        else:
+            self.host = feat_data.pin_memory() if pin_host else feat_data.contiguous()
         idx = torch.from_numpy(np.asarray(buffer_nodes, dtype=np.int64))
         buf = torch.zeros((len(idx), self.ld), dtype=torch.float32)
         buf[:, : self.F] = feat_data[idx]
@@ -80,10 +110,10 @@ class StagePlan:
     own_pos: np.ndarray      # X0 rows filled from this rank's buffer
     own_src: np.ndarray      # their slots in the buffer
     host_pos: np.ndarray     # X0 rows filled from host memory
-    host_rows: torch.Tensor  # pinned (n_host x ld) rows, already gathered on the host
+    host_rows: Optional[torch.Tensor]  # pinned (n_host x ld) rows gathered on the host (None: zero-copy)
     peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
-    pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos)
+    pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos[, host_src])
     peer_meta: Optional[tuple] = None  # PeerExchange.prepare: (send counts, recv counts, want, pos)
 
 
@@ -94,7 +124,9 @@ def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devic
     own_pos = np.flatnonzero(masks[rank]).astype(np.int64)
     own_src = np.asarray(idxs[rank], dtype=np.int64)
     host_pos = np.flatnonzero(host_batch.input_nodes_mask_on_cpu).astype(np.int64)
-    host_rows = store.host_rows_pinned(host_batch.nodes_idx_on_cpu)
+    # zero-copy stores: the GPU reads the rows itself (Stager.issue); else gather them here
+    host_src = np.ascontiguousarray(host_batch.nodes_idx_on_cpu, dtype=np.int64)
+    host_rows = None if store.zero_copy else store.host_rows_pinned(host_src)
     peer_pos, peer_src = [], []
     for j in range(world_size):
         if j == rank:
@@ -104,7 +136,8 @@ def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devic
             peer_pos.append(np.flatnonzero(masks[j]).astype(np.int64))
             peer_src.append(np.asarray(idxs[j], dtype=np.int64))
     cuda = torch.cuda.is_available()
-    pin = tuple(torch.from_numpy(a).pin_memory() if cuda else torch.from_numpy(a) for a in (own_pos, own_src, host_pos))
+    arrs = (own_pos, own_src, host_pos) + ((host_src,) if store.zero_copy else ())
+    pin = tuple(torch.from_numpy(a).pin_memory() if cuda else torch.from_numpy(a) for a in arrs)
     return StagePlan(host_batch.num_input_nodes, own_pos, own_src, host_pos, host_rows, peer_pos, peer_src, pin)
 
 
@@ -139,17 +172,23 @@ class Stager:
         # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
             x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
-            own_pos, own_src, host_pos = (t.to(dev, non_blocking=True) for t in plan.pinned)
+            idx = [t.to(dev, non_blocking=True) for t in plan.pinned]
+            own_pos, own_src, host_pos = idx[:3]
+            nh = len(plan.host_pos)
             if self.timing is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-            host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
+            if plan.host_rows is None:  # zero-copy: the GPU reads the rows from the mapped table
+                host_dev = idx[3]
+                cso.gather_rows_host(self.store.host, host_dev, x0, host_pos, n=nh)
+            else:
+                host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
             if self.timing is not None:
                 e1.record(st)
-                self.timing.append((e0, e1, plan.host_rows.numel() * 4))
+                self.timing.append((e0, e1, nh * self.store.ld * 4))
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
-            if len(plan.host_pos):
-                cso.gather_rows(host_dev, None, x0, host_pos, n=len(plan.host_pos))
+            if nh and plan.host_rows is not None:
+                cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
             extra = ()
             if self.exchange is not None:
                 extra = self.exchange.exchange(plan, x0, self.store)

@@ -154,6 +154,19 @@ int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx
                         float* dst, int64_t ld_dst, const int64_t* dst_idx,
                         int64_t n, int64_t F, void* stream);
 
+/* Zero-copy variant for the non-buffered rows (replaces the pageable
+ * feat_data[idx_cpu].to(device) of main.py:134): `host_src` is host memory registered with
+ * gnn_host_register (pinned, device-mapped); the GPU reads the rows over PCIe, so no host
+ * thread copies them. src_idx / dst_idx are device int64 arrays (NULL = identity). A small
+ * persistent grid keeps the gather's CU footprint low beside the compute stream. */
+int gnn_gather_rows_host_f32(const float* host_src, int64_t ld_src, const int64_t* src_idx,
+                             float* dst, int64_t ld_dst, const int64_t* dst_idx,
+                             int64_t n, int64_t F, void* stream);
+
+/* Pin + map a host range for device access (hipHostRegister, mapped) / undo it. */
+int gnn_host_register(void* host, size_t bytes);
+int gnn_host_unregister(void* host);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,10 @@ def test_argument_validation_without_gpu():
     assert rc == -22 and b"negative" in L.gnn_last_error()
     with pytest.raises(RuntimeError, match="negative size"):
         _lib.check(L.gnn_gather_rows_f32(None, 1, None, None, 1, None, -5, 1, None), "gather")
+    with pytest.raises(RuntimeError, match="negative size"):
+        _lib.check(L.gnn_gather_rows_host_f32(None, 1, None, None, 1, None, -5, 1, None), "gather_host")
+    assert L.gnn_gather_rows_host_f32(None, 8, None, None, 8, None, 0, 8, None) == 0  # empty: no-op
+    assert L.gnn_host_register(None, 0) == -22 and b"NULL" in L.gnn_last_error()
     # F larger than the row stride
     rc = L.gnn_spmm_csr_f32(None, None, None, 4, 4, 0, None, 2, None, 8, 4, None, 0, 0, None)
     assert rc == -22 and b"ldx" in L.gnn_last_error()

@@ -59,3 +59,41 @@ def test_side_stream_batch_matches_compute_stream(dev):
         assert float(l1) == float(l2)
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.equal(p1, p2)
+
+
+def test_zero_copy_host_rows_match_copy_path(dev):
+    """FeatureStore(zero_copy=True): the GPU reads the non-buffered rows from the pinned,
+    device-mapped host table (gnn_gather_rows_host_f32); X0 must be bit-identical to the
+    feature table rows and to the pinned-copy path's X0, pads zero."""
+    lap, labels, train = _setup()
+    N = lap.shape[0]
+    pl = placement.create_buffer_ours(lap, train, 500, [0], 3, alpha=0)
+    feats = torch.randn(N, 37)  # odd width: 8-byte vectors, 64-float padded rows
+    zc = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0, zero_copy=True)
+    cp = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    ld = loader.BatchLoader(lap, labels, train, 800, 128, [1, 1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], rank=0, world_size=1, store=zc, workers=2, seed=3)
+    lbs = list(ld.epoch(1))[:3]
+    ld.close()
+    s_zc, s_cp = staging.Stager(zc), staging.Stager(cp)
+    for lb in lbs:
+        assert lb.plan.host_rows is None and len(lb.plan.host_pos) > 0
+        plan_cp = staging.make_plan(lb.host, cp, 0, 1)
+        x_zc = s_zc.issue(lb.plan).wait()
+        x_cp = s_cp.issue(plan_cp).wait()
+        torch.cuda.synchronize()
+        want = feats[torch.from_numpy(lb.host.input_nodes)]
+        assert torch.equal(x_zc.cpu(), want)
+        assert torch.equal(x_zc.cpu(), x_cp.cpu())
+        full = x_zc.as_strided((x_zc.shape[0], zc.ld), (zc.ld, 1))
+        assert torch.all(full[:, 37:].cpu() == 0)
+
+
+def test_zero_copy_gather_rejects_unregistered_memory(dev):
+    from gnn_amd import custom_sparse_ops as cso
+
+    host = torch.randn(16, 8)  # plain pageable memory, never registered
+    idx = torch.arange(4, device=dev)
+    dst = torch.empty(4, 8, device=dev)
+    with pytest.raises(RuntimeError, match="hipHostGetDevicePointer"):
+        cso.gather_rows_host(host, idx, dst, None)
