@@ -39,6 +39,9 @@ def log(*a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+GRAPH_NAMES = {"reddit": "Reddit", "products": "ogbn-products", "papers": "ogbn-papers100M-scaled", "tiny": "tiny"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -52,7 +55,9 @@ def parse():
     ap.add_argument("--nhid", type=int, default=512)
     ap.add_argument("--buffer-size", type=float, default=0.1)
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--graph", default="reddit", choices=["reddit", "tiny"])
+    ap.add_argument("--graph", default="reddit", choices=["reddit", "products", "papers", "tiny"],
+                    help="synthetic graph shape: reddit (configs 1-2), products (configs 3, 5), papers "
+                         "(config 4's per-batch geometry on a graph scaled to the box), tiny (smoke)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -290,7 +295,8 @@ def main():
     dev = torch.device("cuda", local)
 
     t0 = time.time()
-    spec = graphs.REDDIT if args.graph == "reddit" else graphs.TINY
+    spec = {"reddit": graphs.REDDIT, "products": graphs.PRODUCTS, "papers": graphs.PAPERS_SCALED,
+            "tiny": graphs.TINY}[args.graph]
     A, labels, feats, num_classes, train, valid, test = graphs.make_dataset(spec, seed=0)
     lap = graphs.row_normalize(A)
     lap.sum_duplicates()
@@ -492,9 +498,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (Chung-Lu Reddit-shaped graph, N(0,1) features, random-init GraphSAGE); "
-                    f"{nb} pre-sampled LADIES batches per rank cycled, operands resident in HBM",
-            "config": {"workload": (f"Reddit {'GraphSAGE' if args.model == 'graphsage' else 'GCN'} "
+            "data": f"synthetic (Chung-Lu {spec.name}-shaped graph, N(0,1) features, random-init "
+                    f"{'GraphSAGE' if args.model == 'graphsage' else 'GCN'}); "
+                    f"{nb} pre-sampled {args.sampler} batches per rank cycled, operands resident in HBM",
+            "config": {"workload": (f"{GRAPH_NAMES[args.graph]} {'GraphSAGE' if args.model == 'graphsage' else 'GCN'} "
                                     f"{args.sampler.upper() if args.sampler != 'fastgcn' else 'FastGCN'} "
                                     f"samp_num={args.samp_num} batch_size={args.batch_size}"
                                     + (" (BASELINE config 2)" if (args.model, args.sampler, args.samp_num,

@@ -140,6 +140,33 @@ def test_forward_edge_cases(dev):
     _check_fwd(dev, 64, 40, 26, lens, seed=4)
 
 
+@pytest.mark.parametrize("unit", [0, 1, 4, 64])
+def test_empty_row_runs(dev, unit):
+    """Long runs of empty rows (a FastGCN layer's transpose: 8 k rows, ~2 k nonzeros) at the
+    start, in the middle and at the end — stored by the row units, skipped by the nonzero
+    units — with and without the row-mapped residual."""
+    M, K, F = 8192, 700, 96
+    rng = np.random.default_rng(unit + 5)
+    lens = np.zeros(M, int)
+    lens[3000:3010] = rng.integers(1, 60, 10)          # empty rows 0..2999 before
+    lens[5000] = 400                                     # run of 1,990 empty rows before, a cut row
+    lens[rng.choice(np.arange(5001, 6000), 300, replace=False)] = 1
+    _check_fwd(dev, M, K, F, lens, seed=unit, unit_nnz=unit)  # rows 6000.. empty to the end
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    R = rng.standard_normal((M // 4, F)).astype(np.float32)
+    rmap = np.full(M, -1, np.int32)
+    pick = rng.choice(M, M // 4, replace=False)
+    rmap[pick] = np.arange(M // 4, dtype=np.int32)
+    Yref = O.spmm_f32(rowptr, ocol, oval, X)
+    Yref[pick] += R
+    Y = cso.spmm_csr(op, torch.from_numpy(X).to(dev), unit_nnz=unit, residual=torch.from_numpy(R).to(dev),
+                     rmap=torch.from_numpy(rmap).to(dev))
+    np.testing.assert_allclose(Y.cpu().numpy(), Yref, rtol=RTOL, atol=ATOL)
+
+
 def test_forward_empty_shapes(dev):
     op = _op(dev, np.zeros(1, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32), np.ones(5, np.float32), 0, 5)
     Y = cso.spmm_csr(op, torch.randn(5, 8, device=dev))
