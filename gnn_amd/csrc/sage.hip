@@ -13,6 +13,7 @@
 // workgroup into a slab and then summed over workgroups in a fixed order (deterministic).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
@@ -63,7 +64,9 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, float p) 
 }
 
 __device__ __forceinline__ float elu1(float h) { return h > 0.0f ? h : expm1f(h); }
-__device__ __forceinline__ float elu1_grad(float h) { return h > 0.0f ? 1.0f : expf(h); }
+// d elu(h) / dh from the activation o = elu(h): 1 for h > 0 (o > 0), else exp(h) = o + 1
+// (one rounding of expm1(h) + 1 instead of a second exponential).
+__device__ __forceinline__ float elu1_grad_from_out(float o) { return o > 0.0f ? 1.0f : o + 1.0f; }
 
 // Pre-activation of column c of row r: the linear output plus its bias (when given).
 __device__ __forceinline__ f4 load_h(const float* hB, int64_t ldb, const float* bB, int D1, const float* hW,
@@ -165,8 +168,10 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
     for (int k = 0; k < NV; ++k) {
       const int c = (lane + 64 * k) * 4;
       if (c < D) {
-        h[k] = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
-        const f4 o = f4{elu1(h[k].x), elu1(h[k].y), elu1(h[k].z), elu1(h[k].w)};
+        const f4 hk = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
+        const f4 o = f4{elu1(hk.x), elu1(hk.y), elu1(hk.z), elu1(hk.w)};
+        h[k] = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
+                  elu1_grad_from_out(o.w)};  // h[k] now holds the ELU derivative
         xh[k] = (o - m) * rs;
         f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
         if (training) {
@@ -193,8 +198,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
       const int c = (lane + 64 * k) * 4;
       if (c < D) {
         const f4 dxo = rs * (gx[k] - a - xh[k] * b);
-        const f4 dh = f4{dxo.x * elu1_grad(h[k].x), dxo.y * elu1_grad(h[k].y), dxo.z * elu1_grad(h[k].z),
-                         dxo.w * elu1_grad(h[k].w)};
+        const f4 dh = dxo * h[k];
         dbi[k] += dh;
         if (c < D1) {
           *reinterpret_cast<f4*>(dhB + (int64_t)r * D1 + c) = dh;
@@ -220,35 +224,149 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
   }
 }
 
-// Column sums over the G workgroup partials: a workgroup owns 64 of the NRED*D columns; its
-// 4 waves take interleaved quarters of the partial rows (8 loads in flight per lane), and
-// the quarters are added in a fixed order through LDS (deterministic).
+// Split-row backward (D % 8 == 0, D >= 512): two waves per row, each holding half of it
+// (half the registers: ~2x the rows in flight per CU, the 1-wave form is latency-bound at
+// 3 workgroups per CU); the row sums meet in LDS (half 0 + half 1, fixed order) behind one
+// barrier per row pair, double-buffered by iteration parity.
+constexpr int BWD2_MAX_GRID = 1024;
+
+template <int NVH>
+__global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
+    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb,
+    const float* __restrict__ bB, int D1, const float* __restrict__ hW, int64_t ldw, const float* __restrict__ bW,
+    int D, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd, int M,
+    float p, float inv_keep, uint64_t seed, int training, float* __restrict__ dhB, float* __restrict__ dhW,
+    float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2 row slots][D]
+  __shared__ float rsum[2][4][2];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int slot = w >> 1, half = w & 1;
+  const int Dh = D >> 1;
+  const int cbase = half * Dh;
+  const int cend = half ? D : Dh;
+  f4 ds[NVH], db[NVH], dbi[NVH];
+#pragma unroll
+  for (int k = 0; k < NVH; ++k) {
+    ds[k] = f4(0.0f);
+    db[k] = f4(0.0f);
+    dbi[k] = f4(0.0f);
+  }
+  int it = 0;
+  for (int r0 = blockIdx.x * 2; r0 < M; r0 += gridDim.x * 2, ++it) {
+    const int r = r0 + slot;
+    const bool live = r < M;
+    f4 eg[NVH], xh[NVH], gx[NVH];
+    float a = 0.0f, b = 0.0f;
+    float m = 0.0f, rs = 0.0f;
+    if (live) {
+      m = mean[r];
+      rs = rstd[r];
+    }
+#pragma unroll
+    for (int k = 0; k < NVH; ++k) {
+      const int c = cbase + (lane + 64 * k) * 4;
+      if (live && c < cend) {
+        const f4 hk = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
+        const f4 o = f4{elu1(hk.x), elu1(hk.y), elu1(hk.z), elu1(hk.w)};
+        eg[k] = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
+                   elu1_grad_from_out(o.w)};
+        xh[k] = (o - m) * rs;
+        f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
+        if (training) {
+          const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
+          g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
+          g.y = keep_elem(seed, e + 1, p) ? g.y * inv_keep : 0.0f;
+          g.z = keep_elem(seed, e + 2, p) ? g.z * inv_keep : 0.0f;
+          g.w = keep_elem(seed, e + 3, p) ? g.w * inv_keep : 0.0f;
+        }
+        db[k] += g;
+        ds[k] += g * xh[k];
+        gx[k] = g * *reinterpret_cast<const f4*>(scale + c);
+        const f4 gxx = gx[k] * xh[k];
+        a += (gx[k].x + gx[k].y) + (gx[k].z + gx[k].w);
+        b += (gxx.x + gxx.y) + (gxx.z + gxx.w);
+      } else {
+        eg[k] = xh[k] = gx[k] = f4(0.0f);
+      }
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int buf = it & 1;
+    if (lane == 0) {
+      rsum[buf][w][0] = a;
+      rsum[buf][w][1] = b;
+    }
+    __syncthreads();
+    const float A = (rsum[buf][2 * slot][0] + rsum[buf][2 * slot + 1][0]) / (float)D;
+    const float B = (rsum[buf][2 * slot][1] + rsum[buf][2 * slot + 1][1]) / (float)D;
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < NVH; ++k) {
+        const int c = cbase + (lane + 64 * k) * 4;
+        if (c < cend) {
+          const f4 dh = rs * (gx[k] - A - xh[k] * B) * eg[k];
+          dbi[k] += dh;
+          if (c < D1) {
+            *reinterpret_cast<f4*>(dhB + (int64_t)r * D1 + c) = dh;
+          } else {
+            *reinterpret_cast<f4*>(dhW + (int64_t)r * (D - D1) + (c - D1)) = dh;
+          }
+        }
+      }
+    }
+  }
+  // workgroup column sums -> partial[blockIdx.x][q][D]: slot 0 + slot 1 (fixed order)
+#pragma unroll
+  for (int q = 0; q < NRED; ++q) {
+#pragma unroll
+    for (int k = 0; k < NVH; ++k) {
+      const int c = cbase + (lane + 64 * k) * 4;
+      if (c < cend) *reinterpret_cast<f4*>(red + slot * D + c) = (q == 0) ? ds[k] : (q == 1) ? db[k] : dbi[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256) partial[((int64_t)blockIdx.x * NRED + q) * D + c] = red[c] + red[D + c];
+    __syncthreads();
+  }
+}
+
+// Column sums over the G workgroup partials: a workgroup owns FIN_COLS of the NRED*D
+// columns (192 workgroups at D = 1024, not 48: the sum is latency-bound); thread t sums
+// column t % FIN_COLS over the partial rows g = t / FIN_COLS (mod 16), 4 loads in flight,
+// and the 16 group sums are added in a fixed order through LDS (deterministic).
+constexpr int FIN_COLS = 16;
+
 __global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float* __restrict__ partial, int G, int D,
                                                                      int D1, float* __restrict__ dscale,
                                                                      float* __restrict__ doffset,
                                                                      float* __restrict__ dbB,
                                                                      float* __restrict__ dbW) {
-  __shared__ float qs[4][64];
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;
+  __shared__ float qs[16][FIN_COLS];
+  const int cl = threadIdx.x % FIN_COLS;
+  const int grp = threadIdx.x / FIN_COLS;  // 0..15
+  const int i = blockIdx.x * FIN_COLS + cl;
   float s = 0.0f;
   if (i < NRED * D) {
     const int64_t stride = (int64_t)NRED * D;
-    int g = w;
-    float a[8];
-    for (; g + 28 < G; g += 32) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] = partial[(int64_t)(g + 4 * k) * stride + i];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s += a[k];
+    int g = grp;
+    for (; g + 48 < G; g += 64) {
+      const float a0 = partial[(int64_t)(g + 0) * stride + i];
+      const float a1 = partial[(int64_t)(g + 16) * stride + i];
+      const float a2 = partial[(int64_t)(g + 32) * stride + i];
+      const float a3 = partial[(int64_t)(g + 48) * stride + i];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
     }
-    for (; g < G; g += 4) s += partial[(int64_t)g * stride + i];
+    for (; g < G; g += 16) s += partial[(int64_t)g * stride + i];
   }
-  qs[w][lane] = s;
+  qs[grp][cl] = s;
   __syncthreads();
-  if (w == 0 && i < NRED * D) {
-    const float t = (qs[0][lane] + qs[1][lane]) + (qs[2][lane] + qs[3][lane]);
+  if (grp == 0 && i < NRED * D) {
+    float t = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t += qs[q][cl];
     const int q = i / D, c = i % D;
     if (q == 0) {
       dscale[c] = t;
@@ -280,6 +398,25 @@ FwdFn fwd_fn(int nv) {
     case 8: return &sage_norm_fwd_kernel<8>;
     default: return nullptr;
   }
+}
+
+BwdFn bwd2_fn(int nvh) {
+  switch (nvh) {
+    case 1: return &sage_norm_bwd2_kernel<1>;
+    case 2: return &sage_norm_bwd2_kernel<2>;
+    case 3: return &sage_norm_bwd2_kernel<3>;
+    case 4: return &sage_norm_bwd2_kernel<4>;
+    default: return nullptr;
+  }
+}
+
+// the split-row form applies (and its grid G, which sizes the partial slab)
+bool use_bwd2(int64_t D) { return D % 8 == 0 && D >= 512 && std::getenv("GNN_SAGE_BWD1") == nullptr; }
+
+int64_t bwd_grid(int64_t M, int64_t D) {
+  if (use_bwd2(D)) return std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 2), BWD2_MAX_GRID));
+  const int64_t cap = bwd_grid_cap();
+  return std::max<int64_t>(1, ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap);
 }
 
 BwdFn bwd_fn(int nv) {
@@ -335,8 +472,7 @@ int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float*
 }
 
 size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
-  const int64_t cap = bwd_grid_cap();
-  const int64_t G = M <= 0 ? 1 : (ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap);
+  const int64_t G = M <= 0 ? 1 : bwd_grid(M, D);
   return gnn::align_up((size_t)G * NRED * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
 }
 
@@ -364,16 +500,20 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
   GNN_REQUIRE(D2 == 0 || (uintptr_t)dhW % 16 == 0, "gnn_sage_norm_bwd_f32: dhW not 16-byte aligned");
   GNN_REQUIRE(workspace && workspace_bytes >= gnn_sage_norm_bwd_workspace_bytes(M, D),
               "gnn_sage_norm_bwd_f32: workspace too small");
-  const int nv = (int)ceil_div(D, 256);
-  const int64_t cap = bwd_grid_cap();
-  const int64_t G = ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap;
+  const int64_t G = bwd_grid(M, D);
   const float inv_keep = 1.0f / (1.0f - p_drop);
   float* partial = (float*)workspace;
-  hipLaunchKernelGGL(bwd_fn(nv), dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st, gY, ldg,
-                     hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop,
-                     inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
+  if (use_bwd2(D)) {
+    hipLaunchKernelGGL(bwd2_fn((int)ceil_div(D / 2, 256)), dim3((unsigned)G), dim3(256), (size_t)2 * D * sizeof(float),
+                       st, gY, ldg, hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M,
+                       p_drop, inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
+  } else {
+    hipLaunchKernelGGL(bwd_fn((int)ceil_div(D, 256)), dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st,
+                       gY, ldg, hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop,
+                       inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
+  }
   GNN_LAUNCHED("sage_norm_bwd_kernel");
-  sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(NRED * D, 64)), dim3(256), 0, st>>>(
+  sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(NRED * D, FIN_COLS)), dim3(256), 0, st>>>(
       partial, (int)G, D, (int)D1, dscale, doffset, dbiasB, dbiasW);
   GNN_LAUNCHED("sage_norm_bwd_finalize_kernel");
   return 0;
