@@ -440,3 +440,55 @@ def test_errors(dev):
         cso.spmm_load_balance(A.coalesce().to(dev), torch.randn(3, 2, device=dev).t())
     with pytest.raises(RuntimeError, match="size mismatch"):
         cso.spmm(A.coalesce().to(dev), torch.randn(3, 3, device=dev))
+
+
+def _config2_operand(M, K, nnz_target, rng):
+    """A BASELINE config-2-sized sampled operand (power-law rows, skewed columns), built
+    vectorised: M x K with ~nnz_target unique entries, ascending columns per row."""
+    lens = powerlaw_lens(M, nnz_target / M, 1.3, rng, K)
+    rows = np.repeat(np.arange(M, dtype=np.int64), lens)
+    w = rng.lognormal(0.0, 1.3, K)
+    cols = rng.choice(K, rows.size, p=w / w.sum())
+    key = np.unique(rows * K + cols)
+    r, c = key // K, (key % K).astype(np.int32)
+    rowptr = np.zeros(M + 1, np.int32)
+    rowptr[1:] = np.cumsum(np.bincount(r, minlength=M))
+    full = np.zeros(M + 1, np.int32)
+    full[1:] = np.cumsum(np.diff(rowptr) + rng.integers(0, 4, M) + 1)
+    normfact = rng.uniform(0.25, 8.0, K).astype(np.float32)
+    return full, rowptr, c, normfact
+
+
+def test_config2_full_size_forward_and_backward(dev):
+    """BASELINE config 2 sizes (Reddit LADIES samp 8192, batch 512): the layer-0 forward
+    (15.8 k x 22.2 k, ~1.8 M nonzeros, F = 602 in 608-float rows) and the layer-1 backward
+    (Aᵀ·G with A 8.7 k x 15.8 k, ~0.86 M nonzeros, F = 1024) against the C oracle, plus
+    linearity A·(X + 2Z) = A·X + 2·A·Z at full size."""
+    rng = np.random.default_rng(2024)
+    M, K, F = 15809, 22176, 602
+    full, rowptr, col, nf = _config2_operand(M, K, 1.81e6, rng)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    assert np.array_equal(op.col.cpu().numpy(), ocol) and np.array_equal(op.val.cpu().numpy(), oval)
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    buf = torch.zeros((K, 608), dtype=torch.float32, device=dev)
+    buf[:, :F] = torch.from_numpy(X).to(dev)
+    Y = cso.spmm_csr(op, buf[:, :F])
+    np.testing.assert_allclose(Y.cpu().numpy(), O.spmm_f32(rowptr, ocol, oval, X), rtol=RTOL, atol=ATOL)
+    Z = torch.randn(K, F, device=dev)
+    lhs = cso.spmm_csr(op, buf[:, :F] + 2 * Z)
+    rhs = Y + 2 * cso.spmm_csr(op, Z)
+    scale = cso.spmm_csr(op, buf[:, :F].abs() + 2 * Z.abs())  # |A|·(|X| + 2|Z|) bounds the rounding
+    assert bool(((lhs - rhs).abs() <= 1e-5 * scale + 1e-6).all())
+
+    M1, K1, F1 = 8689, 15809, 1024
+    full, rowptr, col, nf = _config2_operand(M1, K1, 0.86e6, rng)
+    op1 = _op(dev, full, rowptr, col, nf, M1, K1)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    G = rng.standard_normal((M1, F1)).astype(np.float32)
+    dX = cso.spmm_csr(op1.transpose(), torch.from_numpy(G).to(dev))
+    trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K1)
+    t = op1.transpose()
+    assert np.array_equal(t.rowptr.cpu().numpy(), trp) and np.array_equal(t.col.cpu().numpy(), trc)
+    assert np.array_equal(t.val.cpu().numpy(), trv)
+    np.testing.assert_allclose(dX.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
