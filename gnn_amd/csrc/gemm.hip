@@ -253,35 +253,269 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(Batch bt, const
   }
 }
 
-// Workgroup slots of the chip at the kernel's occupancy (2 per CU: 80 KB of LDS each).
-constexpr int64_t SLOTS = 2 * 256;
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores by an exact three-way split ("split3").
+//
+// Every fp32 operand is cut into three bf16 pieces by truncation, x = h + m + l EXACTLY
+// (h keeps the top 8 significant bits, m the next 8 bits of the remainder, l the remaining
+// <= 8 bits), and a·b is accumulated in fp32 as the six largest piece products
+//   h·h + h·m + m·h + h·l + m·m + l·h
+// on v_mfma_f32_32x32x16_bf16 (each bf16 x bf16 product is exact in fp32). The three dropped
+// products (m·l, l·m, l·l) are below 3·2^-24 |a||b| — the size of one fp32 rounding — so the
+// result has fp32-level accuracy (tests/test_gemm_gpu.py bounds it against fp64 with the same
+// tolerance as the f32-input kernel above). Six bf16 MFMAs (6 × 32 cycles per 32×32×16) do
+// the work of eight f32-input ones (8 × 64 cycles): 2.67× the matrix rate.
+//
+// Tiling: 256-thread workgroup = 2 × 2 waves, 128 × 128 output tile, k staged 16 deep in
+// double-buffered LDS (48 KB: three workgroups per CU). Each operand tile is loaded as 8
+// floats of one row per thread — k-contiguous sources by two 16-byte (or four 8-byte) loads,
+// k-major sources by eight 4-byte loads whose wave instruction covers 64 consecutive columns —
+// split into its pieces in registers and stored as three k-contiguous images [128][16] bf16
+// (one 16-byte store per piece; the MFMA operand of lane (r, h) is the 16 bytes at row r,
+// k 8h, read with ds_read_b128 from a bank-swizzled image). Operands are read by buffer loads
+// (per-thread VGPR offset + scalar k offset) two k tiles ahead of the MFMAs.
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+constexpr int S3_BK = 16;                  // k per LDS stage
+constexpr int S3_PIECE = BM * S3_BK;       // bf16 per piece image
+constexpr int S3_OPER = 3 * S3_PIECE;      // bf16 per operand stage
+
+// Buffer resource over one operand (raw, byte offsets; the host guarantees extents < 2^31 B).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t s3_rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+// 8 floats of one operand row (row rr of the tile, k = kh*8 .. kh*8+7 of the stage), by buffer
+// loads whose per-thread part (column / row start) is a fixed VGPR offset and whose k part is
+// a scalar offset: no per-load 64-bit address arithmetic.
+//   k-major source: thread t holds column m = t & 127 (a wave instruction reads 64 consecutive
+//     floats of one k row); the k half kh = t >> 7 is wave-uniform.
+//   k-contiguous source: thread t holds row t >> 1, k half t & 1 (two 16-byte or four 8-byte loads).
+template <bool KMAJ, int VEC, bool GUARD>
+__device__ __forceinline__ void s3_load(__amdgpu_buffer_rsrc_t rs, const float* __restrict__ P, int64_t ld, int voff,
+                                        int r0, int rlim, int k0, int klim, int t, float v[8]) {
+  if constexpr (KMAJ) {
+    const int kb = k0 + __builtin_amdgcn_readfirstlane((t >> 7) * 8);
+    if constexpr (GUARD) {
+      const int m = min(r0 + (t & 127), rlim - 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (kb + i < klim) ? P[(int64_t)(kb + i) * ld + m] : 0.0f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        v[i] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (int)((int64_t)(kb + i) * ld * 4), 0));
+    }
+  } else {
+    if constexpr (GUARD) {
+      const int m = min(r0 + (t >> 1), rlim - 1);
+      const int kb = k0 + (t & 1) * 8;
+      const float* q = P + (int64_t)m * ld + kb;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (kb + i < klim) ? q[i] : 0.0f;
+    } else {
+      const int so = k0 * 4;
+      if constexpr (VEC == 4) {
+        const f4 a = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 0));
+        const f4 b = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, so, 0));
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f2 a = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff + 8 * i, so, 0));
+          v[2 * i] = a.x;
+          v[2 * i + 1] = a.y;
+        }
+      }
+    }
+  }
+}
+
+// The thread's fixed VGPR byte offset for s3_load (rows past the edge clamped to the last row).
+template <bool KMAJ>
+__device__ __forceinline__ int s3_voff(int64_t ld, int r0, int rlim, int t) {
+  if constexpr (KMAJ) return min(r0 + (t & 127), rlim - 1) * 4;
+  else return (int)(((int64_t)min(r0 + (t >> 1), rlim - 1) * ld + (t & 1) * 8) * 4);
+}
+
+// Offset (in bf16 units) of the 16-byte chunk (row, k half h) in a piece image. The half is
+// swizzled by bit 3 of the row so that every 16-lane group of a ds_read_b128 (lanes
+// {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...: MI355X_MICROARCH.md §LDS) covers all 64 banks
+// (unswizzled, rows r and r + 8 of a group share banks: 2-way conflicts, measured).
+__device__ __forceinline__ int s3_chunk(int row, int h) { return (2 * row + (h ^ ((row >> 3) & 1))) * 8; }
+
+// Split 8 floats into their three bf16 pieces and store them into the stage's images.
+template <bool KMAJ>
+__device__ __forceinline__ void s3_store(unsigned short* __restrict__ S, int t, const float v[8]) {
+  const int rr = KMAJ ? (t & 127) : (t >> 1);
+  const int kh = KMAJ ? (t >> 7) : (t & 1);
+  unsigned int h[8], m[8], l[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const unsigned int u = __float_as_uint(v[i]);
+    h[i] = u & 0xffff0000u;
+    const float r = v[i] - __uint_as_float(h[i]);  // exact
+    m[i] = __float_as_uint(r) & 0xffff0000u;
+    l[i] = __float_as_uint(r - __uint_as_float(m[i]));  // exact, <= 8 significant bits
+  }
+  u4v ph, pm, pl;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ph[j] = h[2 * j + 1] | (h[2 * j] >> 16);
+    pm[j] = m[2 * j + 1] | (m[2 * j] >> 16);
+    pl[j] = (l[2 * j + 1] & 0xffff0000u) | (l[2 * j] >> 16);
+  }
+  const int off = s3_chunk(rr, kh);
+  *reinterpret_cast<u4v*>(S + off) = ph;
+  *reinterpret_cast<u4v*>(S + S3_PIECE + off) = pm;
+  *reinterpret_cast<u4v*>(S + 2 * S3_PIECE + off) = pl;
+}
+
+__device__ __forceinline__ bf8v s3_frag(const unsigned short* __restrict__ S, int piece, int row, int h) {
+  return __builtin_bit_cast(bf8v, *reinterpret_cast<const u4v*>(S + piece * S3_PIECE + s3_chunk(row, h)));
+}
+
+// The six piece products of one k16 step into the wave's 2 x 2 accumulators (small terms first).
+__device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, const unsigned short* __restrict__ Sb,
+                                       int ra0, int rb0, int li, int lh, f16v acc[2][2]) {
+  bf8v a[2][3], bb[2][3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a[i][p] = s3_frag(Sa, p, ra0 + i * 32 + li, lh);
+      bb[i][p] = s3_frag(Sb, p, rb0 + i * 32 + li, lh);
+    }
+  constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+  constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][PA[q]], bb[j][PB[q]], acc[i][j], 0, 0, 0);
+}
+
+template <bool AK, bool BKM, int VA, int VB>
+__global__ __launch_bounds__(256) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
+                                                         int64_t ldc, int splits, int klen, float* __restrict__ part,
+                                                         int64_t abytes, int64_t bbytes) {
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][S3_OPER];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int b = blockIdx.z / splits;
+  const int split = blockIdx.z % splits;
+  const int m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+  const int kbeg = split * klen;
+  const int kend = min(K, kbeg + klen);
+  const float* __restrict__ A = bt.A[b];
+  const float* __restrict__ B = bt.B[b];
+  const __amdgpu_buffer_rsrc_t rsa = s3_rsrc(A, abytes), rsb = s3_rsrc(B, bbytes);
+  const int voa = s3_voff<AK>(lda, m0, M, t), vob = s3_voff<BKM>(ldb, n0, N, t);
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f16v(0.0f);
+
+  const int nk = kend > kbeg ? (kend - kbeg + S3_BK - 1) / S3_BK : 0;
+  // Two register sets: tile kt+2's loads are in flight while tile kt is multiplied and tile
+  // kt+1 (loaded one tile earlier) is split into the other LDS stage.
+  float ra[2][8], rb[2][8];
+  auto load_ab = [&](int kt, float(&xa)[8], float(&xb)[8]) {
+    if (kt >= nk) return;
+    const int k0 = kbeg + kt * S3_BK;
+    if (k0 + S3_BK <= kend) {
+      s3_load<AK, VA, false>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
+      s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
+    } else {
+      s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
+      s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
+    }
+  };
+  auto store_ab = [&](int kt, int stage, const float(&xa)[8], const float(&xb)[8]) {
+    if (kt >= nk) return;
+    s3_store<AK>(As[stage], t, xa);
+    s3_store<BKM>(Bs[stage], t, xb);
+  };
+  const int li = lane & 31, lh = lane >> 5;
+  load_ab(0, ra[0], rb[0]);
+  load_ab(1, ra[1], rb[1]);
+  store_ab(0, 0, ra[0], rb[0]);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    // tile kt from stage 0; tile kt+1 (set 1) -> stage 1; set 0 <- tile kt+2
+    load_ab(kt + 2, ra[0], rb[0]);
+    s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+    store_ab(kt + 1, 1, ra[1], rb[1]);
+    __syncthreads();
+    // tile kt+1 from stage 1; tile kt+2 (set 0) -> stage 0; set 1 <- tile kt+3
+    load_ab(kt + 3, ra[1], rb[1]);
+    s3_mma(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
+    store_ab(kt + 2, 0, ra[0], rb[0]);
+    __syncthreads();
+  }
+  if (kt < nk) s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);  // odd tile count: the last tile
+
+  float* __restrict__ Cb;
+  int64_t ldo;
+  if (splits > 1) {
+    Cb = part + (int64_t)blockIdx.z * M * N;
+    ldo = N;
+  } else {
+    Cb = bt.C[b];
+    ldo = ldc;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + li;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cb[(int64_t)m * ldo + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+// Workgroup slots of the chip at each kernel's occupancy: f32-input kernel 2 per CU (80 KB of
+// LDS each), split3 kernel 3 per CU (48 KB).
+constexpr int64_t SLOTS_F32 = 2 * 256;
+constexpr int64_t SLOTS_S3 = 3 * 256;
 
 // Split count: the weight-gradient shapes have few output tiles and a long k, so split k
 // until the tiles x splits fill the slots once — never past them: a second, nearly empty
 // round of workgroups costs almost a full round (measured: 40 tiles x 12 splits = 480
 // workgroups 190 µs, x 13 = 520 workgroups 255 µs). Each split keeps >= 256 of k.
-int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch) {
+int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch, int64_t slots) {
   if (const char* e = getenv("GNN_GEMM_SPLITS")) return std::max(1, atoi(e));  // experiments
   const int64_t tiles = ceil_div(M, (int64_t)BM) * ceil_div(N, (int64_t)BN) * nbatch;
-  if (tiles * 2 > SLOTS) return 1;
-  int64_t s = SLOTS / tiles;
+  if (tiles * 2 > slots) return 1;
+  int64_t s = slots / tiles;
   s = std::min<int64_t>(s, std::max<int64_t>(1, K / 256));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
-}  // namespace
+enum Algo { ALGO_F32 = 0, ALGO_S3 = 1 };
 
-extern "C" {
+int64_t slots_of(int algo) { return algo == ALGO_S3 ? SLOTS_S3 : SLOTS_F32; }
 
-size_t gnn_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch) {
-  if (M <= 0 || N <= 0 || K <= 0 || nbatch <= 0) return 0;
-  const int s = pick_splits(M, N, K, nbatch);
-  return s > 1 ? (size_t)s * nbatch * M * N * sizeof(float) : 0;
-}
-
-int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
-                 int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
-                 size_t workspace_bytes, void* stream) {
+int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
+             int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
+             size_t workspace_bytes, void* stream) {
   GNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gnn_gemm_f32: negative size");
   GNN_REQUIRE(M < INT_MAX && N < INT_MAX && K < INT_MAX, "gnn_gemm_f32: sizes must be < 2^31");
   GNN_REQUIRE(nbatch >= 1 && nbatch <= MAX_BATCH, "gnn_gemm_f32: nbatch must be 1..%d", MAX_BATCH);
@@ -301,10 +535,15 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
     bt.B[b] = B[b];
     bt.C[b] = C[b];
   }
+  // split3 addresses operands by 32-bit buffer offsets: operands of >= 2 GiB take the f32-input kernel
+  const int64_t abytes = K == 0 ? 0 : ((a_kmajor ? K : M) - 1) * lda * 4 + (a_kmajor ? M : K) * 4;
+  const int64_t bbytes = K == 0 ? 0 : ((b_kmajor ? K : N) - 1) * ldb * 4 + (b_kmajor ? N : K) * 4;
+  if (algo == ALGO_S3 && (abytes >= INT_MAX || bbytes >= INT_MAX)) algo = ALGO_F32;
   hipStream_t st = (hipStream_t)stream;
-  const int splits = K == 0 ? 1 : pick_splits(M, N, K, nbatch);
-  int bkt = 32;
-  if (const char* e = getenv("GNN_GEMM_BKT")) bkt = atoi(e) == 16 ? 16 : 32;  // experiments
+  const int splits = K == 0 ? 1 : pick_splits(M, N, K, nbatch, slots_of(algo));
+  int bkt = algo == ALGO_S3 ? S3_BK : 32;
+  if (algo == ALGO_F32)
+    if (const char* e = getenv("GNN_GEMM_BKT")) bkt = atoi(e) == 16 ? 16 : 32;  // experiments
   const int klen = splits > 1 ? (int)(ceil_div(ceil_div(K, (int64_t)splits), (int64_t)bkt) * bkt) : (int)K;
   if (splits > 1) {
     const size_t need = (size_t)splits * nbatch * M * N * sizeof(float);
@@ -315,7 +554,10 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
   float* part = (float*)workspace;
 #define GNN_GEMM_LAUNCH(AK, BK, VA, VB)                                                                     \
   do {                                                                                                        \
-    if (bkt == 16)                                                                                            \
+    if (algo == ALGO_S3)                                                                                      \
+      gemm_s3_kernel<AK, BK, VA, VB><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc,  \
+                                                                 splits, klen, part, abytes, bbytes);         \
+    else if (bkt == 16)                                                                                       \
       gemm_f32_kernel<AK, BK, VA, VB, 16>                                                                     \
           <<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc, splits, klen, part);        \
     else                                                                                                      \
@@ -335,7 +577,7 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
   else GNN_GEMM_V(false, false);
 #undef GNN_GEMM_V
 #undef GNN_GEMM_LAUNCH
-  GNN_LAUNCHED("gemm_f32_kernel");
+  GNN_LAUNCHED(algo == ALGO_S3 ? "gemm_s3_kernel" : "gemm_f32_kernel");
   if (splits > 1) {
     const int64_t total = (int64_t)M * N * nbatch;
     const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total, (int64_t)256), 2048);
@@ -343,6 +585,38 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
     GNN_LAUNCHED("gemm_splitk_reduce_kernel");
   }
   return 0;
+}
+
+size_t workspace_bytes_of(int algo, int64_t M, int64_t N, int64_t K, int nbatch) {
+  if (M <= 0 || N <= 0 || K <= 0 || nbatch <= 0) return 0;
+  const int s = pick_splits(M, N, K, nbatch, slots_of(algo));
+  return s > 1 ? (size_t)s * nbatch * M * N * sizeof(float) : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gnn_gemm_f32_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch) {
+  return workspace_bytes_of(ALGO_F32, M, N, K, nbatch);
+}
+
+int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
+                 int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
+                 size_t workspace_bytes, void* stream) {
+  return gemm_run(ALGO_F32, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
+                  stream);
+}
+
+size_t gnn_gemm_f32_split3_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch) {
+  return workspace_bytes_of(ALGO_S3, M, N, K, nbatch);
+}
+
+int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                        const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                        int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_run(ALGO_S3, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
+                  stream);
 }
 
 }  // extern "C"

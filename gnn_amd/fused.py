@@ -11,6 +11,7 @@ torch's Philox stream (same distribution).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -145,21 +146,39 @@ def _ld(t: torch.Tensor) -> int:
     return t.stride(0) if t.shape[0] > 1 else t.shape[1] + (t.shape[1] & 1)
 
 
-def gemm(a_kmajor: bool, b_kmajor: bool, As, Bs, M: int, N: int, K: int):
-    """Batched fp32 MFMA GEMM (gnn_gemm_f32): C[b] = A[b]·B[b] with the layouts of
-    include/gnn_layers.h; all problems share shapes and row strides. Returns new (M x N)
-    tensors."""
+GEMM_ALGOS = ("split3", "f32")
+
+
+def gemm_algo() -> str:
+    """The fp32 GEMM kernel (include/gnn_layers.h): "split3" (bf16 matrix cores on an exact
+    three-way split of every operand, six products, fp32 accumulation) or "f32" (f32-input
+    MFMA). GNN_GEMM_ALGO overrides the default."""
+    a = os.environ.get("GNN_GEMM_ALGO", "split3")
+    if a not in GEMM_ALGOS:
+        raise RuntimeError(f"GNN_GEMM_ALGO must be one of {GEMM_ALGOS}, got {a!r}")
+    return a
+
+
+def gemm(a_kmajor: bool, b_kmajor: bool, As, Bs, M: int, N: int, K: int, algo: Optional[str] = None):
+    """Batched fp32 GEMM on the matrix cores (gnn_gemm_f32 / gnn_gemm_f32_split3):
+    C[b] = A[b]·B[b] with the layouts of include/gnn_layers.h; all problems share shapes and
+    row strides. Returns new (M x N) tensors."""
     import ctypes
 
+    algo = algo or gemm_algo()
     dev = As[0].device
     nb = len(As)
     Cs = [torch.empty((M, N), dtype=torch.float32, device=dev) for _ in range(nb)]
     L = _lib.lib()
-    wsb = L.gnn_gemm_f32_workspace_bytes(M, N, K, nb)
+    if algo == "split3":
+        wsf, fn, name = L.gnn_gemm_f32_split3_workspace_bytes, L.gnn_gemm_f32_split3, "gnn_gemm_f32_split3"
+    else:
+        wsf, fn, name = L.gnn_gemm_f32_workspace_bytes, L.gnn_gemm_f32, "gnn_gemm_f32"
+    wsb = wsf(M, N, K, nb)
     ws = torch.empty(wsb, dtype=torch.uint8, device=dev) if wsb else None
     arr = lambda ts: (ctypes.c_void_p * nb)(*[t.data_ptr() for t in ts])
-    _lib.check(L.gnn_gemm_f32(int(a_kmajor), int(b_kmajor), M, N, K, nb, arr(As), _ld(As[0]), arr(Bs), _ld(Bs[0]),
-                              arr(Cs), N, _ptr(ws), wsb, _stream(dev)), "gnn_gemm_f32")
+    _lib.check(fn(int(a_kmajor), int(b_kmajor), M, N, K, nb, arr(As), _ld(As[0]), arr(Bs), _ld(Bs[0]),
+                  arr(Cs), N, _ptr(ws), wsb, _stream(dev)), name)
     return Cs
 
 
@@ -167,10 +186,13 @@ _GEMM_SLOTS = 512  # workgroup slots of the MFMA kernel (2 per CU, 256 CUs): gem
 
 
 def _mfma_fills(M: int, N: int, nb: int) -> bool:
-    """Whether an unsplit MFMA GEMM of nb (M x N) problems fills its workgroup rounds
-    (>= 90 %). Measured on the layer shapes: the kernel beats the vendor GEMM when it does
-    (15.8k x 602 -> 512 pair: 175 vs 189 µs) and loses when a last round runs half empty
-    (8.7k x 1024 -> 512 pair: 202 vs 171 µs); weight gradients are split to fill exactly."""
+    """Whether our GEMM takes an unsplit (M x N) x nb product. split3 always does: it beats
+    the vendor GEMM on every layer shape (scripts/gemm_bench.py: 117-150 µs per pair against
+    160-256). The f32-input kernel only when it fills its workgroup rounds (>= 90 %):
+    measured, it beats the vendor GEMM when it does (15.8k x 602 -> 512 pair: 175 vs 189 µs)
+    and loses when a last round runs half empty (8.7k x 1024 -> 512 pair: 202 vs 171 µs)."""
+    if gemm_algo() == "split3":
+        return True
     tiles = -(-M // 128) * -(-N // 128) * nb
     rounds = -(-tiles // _GEMM_SLOTS)
     return tiles >= 0.9 * rounds * _GEMM_SLOTS
@@ -216,7 +238,7 @@ class LinearPairFn(torch.autograd.Function):
                 dxs = [torch.mm(g, W) for g, W in zip(gs, Ws)]
         dWs = [None] * n
         if any(ctx.needs_input_grad[1 + n:]):
-            if ok and K % 128:  # split over the sampled rows to fill the chip (gemm.hip pick_splits)
+            if ok and (K % 128 or gemm_algo() == "split3"):  # split over the sampled rows (gemm.hip pick_splits)
                 # Measured (scripts/gemm_sweep.py, in the step): for 602 features the vendor
                 # kernels run at 66 TF/s (145 µs per product) against 95 µs here; for the
                 # 1024-wide layers hipBLASLt's tiles fit exactly and it is faster (79 vs 93 µs).

@@ -59,6 +59,17 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
                  int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
                  size_t workspace_bytes, void* stream);
 
+/* The same contract on the bf16 matrix cores ("split3", gemm.hip): every fp32 operand is cut
+ * EXACTLY into three bf16 pieces by truncation (x = h + m + l) and each output accumulates in
+ * fp32 the six largest piece products h·h + h·m + m·h + h·l + m·m + l·h per k (each exact in
+ * fp32); the dropped products are below 3·2^-24·|a||b|, i.e. fp32-level accuracy (bounded
+ * against fp64 by the same tolerance as gnn_gemm_f32 in tests/test_gemm_gpu.py), at 2.67x the
+ * f32-input matrix rate. Deterministic (fixed accumulation order, k-splits added in order). */
+size_t gnn_gemm_f32_split3_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch);
+int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                        const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                        int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Classifier head + loss (head.hip). Replaces GNN.forward's tail (models.py:90-97:
  * F.normalize(x, 2, 1) -> dropout(p) -> nn.Linear(D, C)) and utils.loss with sigmoid_loss

@@ -33,7 +33,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     variants = os.environ.get("VARIANTS", "-").split(";")
-    knobs = ("GNN_GEMM_PF", "GNN_GEMM_XCD")
+    knobs = ("GNN_GEMM_PF", "GNN_GEMM_XCD", "GNN_GEMM_ALGO")
     res = []
     # (name, a_kmajor, b_kmajor, M, N, K, A (as stored), B (as stored)) for the pair of a layer
     M0, M1 = 15809, 8689
