@@ -400,8 +400,9 @@ __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, co
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][PA[q]], bb[j][PB[q]], acc[i][j], 0, 0, 0);
 }
 
+// three workgroups per CU: LDS 48 KB each, registers capped at 168 (3 waves per SIMD)
 template <bool AK, bool BKM, int VA, int VB>
-__global__ __launch_bounds__(256) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
                                                          int64_t ldc, int splits, int klen, float* __restrict__ part,
                                                          int64_t abytes, int64_t bbytes) {
   __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
@@ -427,45 +428,55 @@ __global__ __launch_bounds__(256) void gemm_s3_kernel(Batch bt, int M, int N, in
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f16v(0.0f);
 
-  const int nk = kend > kbeg ? (kend - kbeg + S3_BK - 1) / S3_BK : 0;
   // Two register sets: tile kt+2's loads are in flight while tile kt is multiplied and tile
   // kt+1 (loaded one tile earlier) is split into the other LDS stage.
   float ra[2][8], rb[2][8];
+  // The main loop runs over the full k tiles with branch-free loads: a prefetch past the last
+  // full tile re-reads that tile (never multiplied). A divergent guarded load inside the loop
+  // made the compiler join two register sets and wait for ALL loads (vmcnt(0)) before the
+  // MFMAs, i.e. no prefetch at all. The k tail (K % 16) runs once after the loop.
+  const int nfull = (kend - kbeg) / S3_BK;
   auto load_ab = [&](int kt, float(&xa)[8], float(&xb)[8]) {
-    if (kt >= nk) return;
-    const int k0 = kbeg + kt * S3_BK;
-    if (k0 + S3_BK <= kend) {
-      s3_load<AK, VA, false>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
-      s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
-    } else {
-      s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
-      s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
-    }
+    const int k0 = kbeg + min(kt, nfull - 1) * S3_BK;
+    s3_load<AK, VA, false>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
+    s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
   };
-  auto store_ab = [&](int kt, int stage, const float(&xa)[8], const float(&xb)[8]) {
-    if (kt >= nk) return;
+  auto store_ab = [&](int stage, const float(&xa)[8], const float(&xb)[8]) {
     s3_store<AK>(As[stage], t, xa);
     s3_store<BKM>(Bs[stage], t, xb);
   };
   const int li = lane & 31, lh = lane >> 5;
-  load_ab(0, ra[0], rb[0]);
-  load_ab(1, ra[1], rb[1]);
-  store_ab(0, 0, ra[0], rb[0]);
-  __syncthreads();
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    // tile kt from stage 0; tile kt+1 (set 1) -> stage 1; set 0 <- tile kt+2
-    load_ab(kt + 2, ra[0], rb[0]);
-    s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
-    store_ab(kt + 1, 1, ra[1], rb[1]);
+  if (nfull > 0) {
+    load_ab(0, ra[0], rb[0]);
+    load_ab(1, ra[1], rb[1]);
+    store_ab(0, ra[0], rb[0]);
     __syncthreads();
-    // tile kt+1 from stage 1; tile kt+2 (set 0) -> stage 0; set 1 <- tile kt+3
-    load_ab(kt + 3, ra[1], rb[1]);
-    s3_mma(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
-    store_ab(kt + 2, 0, ra[0], rb[0]);
-    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nfull; kt += 2) {
+      // tile kt from stage 0; tile kt+1 (set 1) -> stage 1; set 0 <- tile kt+2
+      load_ab(kt + 2, ra[0], rb[0]);
+      s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      store_ab(1, ra[1], rb[1]);
+      __syncthreads();
+      // tile kt+1 from stage 1; tile kt+2 (set 0) -> stage 0; set 1 <- tile kt+3
+      load_ab(kt + 3, ra[1], rb[1]);
+      s3_mma(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
+      store_ab(0, ra[0], rb[0]);
+      __syncthreads();
+    }
+    if (nfull & 1) {  // odd count: the last full tile is in stage 0
+      s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      __syncthreads();
+    }
   }
-  if (kt < nk) s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);  // odd tile count: the last tile
+  if (kbeg + nfull * S3_BK < kend) {  // k tail
+    const int k0 = kbeg + nfull * S3_BK;
+    s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0]);
+    s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, rb[0]);
+    store_ab(0, ra[0], rb[0]);
+    __syncthreads();
+    s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+  }
 
   float* __restrict__ Cb;
   int64_t ldo;

@@ -186,14 +186,17 @@ _GEMM_SLOTS = 512  # workgroup slots of the MFMA kernel (2 per CU, 256 CUs): gem
 
 
 def _mfma_fills(M: int, N: int, nb: int) -> bool:
-    """Whether our GEMM takes an unsplit (M x N) x nb product. split3 always does: it beats
-    the vendor GEMM on every layer shape (scripts/gemm_bench.py: 117-150 µs per pair against
-    160-256). The f32-input kernel only when it fills its workgroup rounds (>= 90 %):
+    """Whether our GEMM takes an unsplit (M x N) x nb product. split3 does when the tiles
+    cover the CUs: it beats the vendor GEMM on every such layer shape (scripts/gemm_bench.py:
+    116-150 µs per pair against 160-256). The f32-input kernel only when it fills its
+    workgroup rounds (>= 90 %):
     measured, it beats the vendor GEMM when it does (15.8k x 602 -> 512 pair: 175 vs 189 µs)
     and loses when a last round runs half empty (8.7k x 1024 -> 512 pair: 202 vs 171 µs)."""
-    if gemm_algo() == "split3":
-        return True
     tiles = -(-M // 128) * -(-N // 128) * nb
+    if gemm_algo() == "split3":
+        # at least one 128 x 128 tile per CU: the layer-2 products (512 rows: 32-64 tiles)
+        # run 22-31 µs here against ~10 µs in the vendor's small-tile kernels
+        return tiles >= 256
     rounds = -(-tiles // _GEMM_SLOTS)
     return tiles >= 0.9 * rounds * _GEMM_SLOTS
 
