@@ -1023,8 +1023,26 @@ int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
   return 1;
 }
 
+// About 2.4 rows' worth of nonzeros as a power of two in [16, 256] (see default_unit).
+int64_t row_unit(int64_t M, int64_t nnz) {
+  int64_t s = 256;
+  if (M > 0) {
+    const double want = 2.4 * (double)nnz / (double)M;
+    while (s > 16 && (double)s > want * 1.41421356) s >>= 1;
+  }
+  return s;
+}
+
+// Small operands (fewer than 2048 row-sized units) take their parallelism from 256-float
+// column tiles before cutting rows into pieces: the layer-2 forward (512 rows of ~30
+// nonzeros, F = 1024) had 2048 units of 8 nonzeros, every row cut and recombined (14 + 17 us).
+// (Operands with < 16 nonzeros per row keep their two-rows-per-unit path.)
+int64_t small_tiles(int64_t M, int64_t nnz, int64_t F) {
+  if (F < 512 || nnz <= 0 || nnz < 16 * M || ceil_div(nnz, row_unit(M, nnz)) >= 2048) return 1;
+  return std::min<int64_t>(F / 256, 8);
+}
+
 int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
-  (void)F;
   // Units are equal-sized (S nonzeros), which balances power-law rows by construction.
   // Measured on the Reddit LADIES layers (scripts/spmm_microbench.py, with L2 column
   // tiles): S = 256 is the sweet spot between per-row flush/search overhead (small S) and
@@ -1035,12 +1053,9 @@ int64_t default_unit(int64_t M, int64_t nnz, int64_t F) {
   // About 2.4 rows per unit, as a power of two in [16, 256]: the layer-1 backward operand
   // (54 nonzeros per row) 199 us at S = 128 vs 209 at 256; the forward operands (98-114 per
   // row) keep 256.
-  int64_t s = 256;
-  if (M > 0) {
-    const double want = 2.4 * (double)nnz / (double)M;
-    while (s > 16 && (double)s > want * 1.41421356) s >>= 1;
-  }
-  if (ceil_div(nnz, s) < 2048) s = ceil_div(nnz, 2048);
+  int64_t s = row_unit(M, nnz);
+  const int64_t t = small_tiles(M, nnz, F);
+  if (ceil_div(nnz, s) * t < 2048) s = ceil_div(nnz * t, 2048);
   if (s < 16) s = 16;
   if (M > 0 && nnz < 16 * M) {
     const int64_t r = 2 * nnz / M;
@@ -1084,6 +1099,15 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
       c.nj = per >= 64 ? (int)(per / 64) : 1;
       if (c.nj > 8) c.nj = 8;
       c.tiles = (int)ceil_div(F, (int64_t)c.vw * c.g * c.nj);
+    }
+  }
+  // Small operands: 256-float column tiles (G = 64, one chunk) for parallelism (small_tiles).
+  if (c.vw == 4 && c.tiles == 1) {
+    const int64_t t = small_tiles(M, nnz, F);
+    if (t > 1) {
+      c.g = 64;
+      c.nj = 1;
+      c.tiles = (int)ceil_div(F, (int64_t)256);
     }
   }
   // Experiment override (benchmarks only): GNN_SPMM_G / GNN_SPMM_NJ force the lane group

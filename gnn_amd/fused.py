@@ -241,11 +241,17 @@ class LinearPairFn(torch.autograd.Function):
                 dxs = [torch.mm(g, W) for g, W in zip(gs, Ws)]
         dWs = [None] * n
         if any(ctx.needs_input_grad[1 + n:]):
-            if ok and (K % 128 or gemm_algo() == "split3"):  # split over the sampled rows (gemm.hip pick_splits)
+            # split over the sampled rows (gemm.hip pick_splits); split3 from 2048 rows (the
+            # layer-2 weight gradient, 512 rows: 19 + 5 µs here vs ~7 µs in the vendor GEMM)
+            if ok and ((gemm_algo() == "split3" and M >= 2048) or (gemm_algo() == "f32" and K % 128)):
                 # Measured (scripts/gemm_sweep.py, in the step): for 602 features the vendor
                 # kernels run at 66 TF/s (145 µs per product) against 95 µs here; for the
                 # 1024-wide layers hipBLASLt's tiles fit exactly and it is faster (79 vs 93 µs).
                 dWs = gemm(True, True, gs, xs, N, K, M)
+            elif gemm_algo() == "split3":
+                # small products on torch's default BLAS: switching the preferred library per
+                # call cost ~0.5 ms of host time per step (host-issue bound steps, measured)
+                dWs = [torch.mm(g.t(), x) for g, x in zip(gs, xs)]
             else:
                 with _BlasLibrary("cublaslt"):
                     dWs = [torch.mm(g.t(), x) for g, x in zip(gs, xs)]

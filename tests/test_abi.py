@@ -101,8 +101,9 @@ def test_workspace_and_config():
     assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 32, 1, 8)
     c = spmm_config(15768, 1821171, 604, K=22153, ldx=604, ldy=604)  # layer 0, padded rows
     assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 16, 1, 10)
-    c = spmm_config(512, 14876, 1024, K=8680)  # little reuse: one tile
-    assert c["tiles"] == 1
+    c = spmm_config(512, 14876, 1024, K=8680)  # small operand: 256-float tiles, rows left whole
+    assert (c["vw"], c["g"], c["nj"], c["tiles"]) == (4, 64, 1, 4)
+    assert L.gnn_spmm_default_unit_nnz(512, 14876, 1024) == 30  # 2048 waves over 4 tiles
     assert L.gnn_csr_transpose_workspace_bytes(10, 1000, 50) >= 4000
     assert L.gnn_segsort_workspace_bytes(100) >= 800
 
