@@ -404,17 +404,31 @@ __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, co
 template <bool AK, bool BKM, int VA, int VB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
                                                          int64_t ldc, int splits, int klen, float* __restrict__ part,
-                                                         int64_t abytes, int64_t bbytes) {
+                                                         int64_t abytes, int64_t bbytes, int xcd_map) {
   __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
   __shared__ __attribute__((aligned(16))) unsigned short Bs[2][S3_OPER];
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wid = t >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int b = blockIdx.z / splits;
-  const int split = blockIdx.z % splits;
-  const int m0 = blockIdx.y * BM;
-  const int n0 = blockIdx.x * BN;
+  // Tile of this workgroup. xcd_map: consecutive tiles (the n tiles of one m row panel)
+  // go to one XCD (workgroups are dealt to the 8 XCDs round-robin), so a row panel of A is
+  // fetched into one L2 instead of up to four.
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (xcd_map) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int per = total >> 3;
+    const int lg = hw < per * 8 ? (hw & 7) * per + (hw >> 3) : hw;
+    tx = lg % gx;
+    ty = (lg / gx) % gy;
+    tz = lg / (gx * gy);
+  }
+  const int b = tz / splits;
+  const int split = tz % splits;
+  const int m0 = ty * BM;
+  const int n0 = tx * BN;
   const int kbeg = split * klen;
   const int kend = min(K, kbeg + klen);
   const float* __restrict__ A = bt.A[b];
@@ -481,7 +495,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   float* __restrict__ Cb;
   int64_t ldo;
   if (splits > 1) {
-    Cb = part + (int64_t)blockIdx.z * M * N;
+    Cb = part + (int64_t)tz * M * N;
     ldo = N;
   } else {
     Cb = bt.C[b];
@@ -552,6 +566,9 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   if (algo == ALGO_S3 && (abytes >= INT_MAX || bbytes >= INT_MAX)) algo = ALGO_F32;
   hipStream_t st = (hipStream_t)stream;
   const int splits = K == 0 ? 1 : pick_splits(M, N, K, nbatch, slots_of(algo));
+  // XCD-aware tile map for split3 (2-8 % per layer pair, scripts/gemm_bench.py); GNN_GEMM_XCD=0 turns it off
+  int xcdm = 1;
+  if (const char* e = getenv("GNN_GEMM_XCD")) xcdm = atoi(e) != 0;
   int bkt = algo == ALGO_S3 ? S3_BK : 32;
   if (algo == ALGO_F32)
     if (const char* e = getenv("GNN_GEMM_BKT")) bkt = atoi(e) == 16 ? 16 : 32;  // experiments
@@ -567,7 +584,7 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   do {                                                                                                        \
     if (algo == ALGO_S3)                                                                                      \
       gemm_s3_kernel<AK, BK, VA, VB><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc,  \
-                                                                 splits, klen, part, abytes, bbytes);         \
+                                                                 splits, klen, part, abytes, bbytes, xcdm);   \
     else if (bkt == 16)                                                                                       \
       gemm_f32_kernel<AK, BK, VA, VB, 16>                                                                     \
           <<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc, splits, klen, part);        \
