@@ -238,6 +238,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(Batch bt, int M, int N, i
   }
 }
 
+// C[b] = sum over splits of the partial tiles, in split order; 4 consecutive outputs per thread
+// (C rows contiguous: ldc == N, M*N % 4 == 0, 16-byte aligned).
+__global__ __launch_bounds__(256) void gemm_splitk_reduce4_kernel(Batch bt, const float* __restrict__ part, int64_t MN,
+                                                                  int splits, int nbatch) {
+  const int64_t n4 = MN / 4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4 * nbatch; e += (int64_t)gridDim.x * 256) {
+    const int b = (int)(e / n4);
+    const int64_t o = (e - (int64_t)b * n4) * 4;
+    const float* p = part + (int64_t)b * splits * MN + o;
+    f4 acc = *reinterpret_cast<const f4*>(p);
+    for (int q = 1; q < splits; ++q) acc += *reinterpret_cast<const f4*>(p + (int64_t)q * MN);
+    *reinterpret_cast<f4*>(bt.C[b] + o) = acc;
+  }
+}
+
 // C[b] = sum over splits of the partial tiles, in split order.
 __global__ __launch_bounds__(256) void gemm_splitk_reduce_kernel(Batch bt, const float* __restrict__ part, int M, int N,
                                                                  int64_t ldc, int splits, int nbatch) {
@@ -609,9 +624,17 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   GNN_LAUNCHED(algo == ALGO_S3 ? "gemm_s3_kernel" : "gemm_f32_kernel");
   if (splits > 1) {
     const int64_t total = (int64_t)M * N * nbatch;
-    const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total, (int64_t)256), 2048);
-    gemm_splitk_reduce_kernel<<<dim3(g), dim3(256), 0, st>>>(bt, part, (int)M, (int)N, ldc, splits, nbatch);
-    GNN_LAUNCHED("gemm_splitk_reduce_kernel");
+    bool vec4 = ldc == N && (M * N) % 4 == 0;
+    for (int b = 0; b < nbatch; ++b) vec4 = vec4 && (uintptr_t)C[b] % 16 == 0;
+    if (vec4) {
+      const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total / 4, (int64_t)256), 2048);
+      gemm_splitk_reduce4_kernel<<<dim3(g), dim3(256), 0, st>>>(bt, part, M * N, splits, nbatch);
+      GNN_LAUNCHED("gemm_splitk_reduce4_kernel");
+    } else {
+      const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total, (int64_t)256), 2048);
+      gemm_splitk_reduce_kernel<<<dim3(g), dim3(256), 0, st>>>(bt, part, (int)M, (int)N, ldc, splits, nbatch);
+      GNN_LAUNCHED("gemm_splitk_reduce_kernel");
+    }
   }
   return 0;
 }
