@@ -337,6 +337,7 @@ def main():
     log(f"setup done ({time.time() - t0:.1f}s); params={trainer.num_params}")
 
     nb = len(dbatches)
+    retire = staging.Retirement()
 
     def pipeline(next_item, steps):
         """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
@@ -346,9 +347,10 @@ def main():
         staged = stager.issue(*next_item())
         for i in range(steps):
             staged_next = stager.issue(*next_item()) if i + 1 < steps else None
-            x0 = staged.wait()
+            x0 = staged.wait(retire)
             db = staged.batch
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
+            retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
             staged = staged_next
         return loss
 
@@ -369,9 +371,11 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    retire.wait_s = 0.0
     t_start = time.perf_counter()
     loss = run(args.steps, args.warmup)
-    t_issued = time.perf_counter()  # host done issuing (GPU-bound runs return early)
+    # host time to issue the steps, without the waits that keep it <= 3 steps ahead of the GPU
+    t_issued = time.perf_counter() - retire.wait_s
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

@@ -211,14 +211,52 @@ class StagedX0:
         # its operands as built by this issue (a later issue may rebuild the same batch)
         self.adjs = list(batch.adjs) if batch is not None and batch.adjs is not None else None
 
-    def wait(self) -> torch.Tensor:
-        """Make the current stream wait for the staging and return the (n x F) view."""
+    def wait(self, retire: Optional["Retirement"] = None) -> torch.Tensor:
+        """Make the current stream wait for the staging and return the (n x F) view. The
+        staged buffers were allocated on the staging stream and are read on this one: either
+        each is marked with record_stream (default), or ``retire`` keeps them alive until the
+        consuming step has run on the GPU (one event instead of ~40 record_stream calls)."""
         cur = torch.cuda.current_stream(self._x0.device)
         cur.wait_event(self.event)
-        self._x0.record_stream(cur)
-        for t in self._keep:
-            t.record_stream(cur)
+        if retire is None:
+            self._x0.record_stream(cur)
+            for t in self._keep:
+                t.record_stream(cur)
         return self._x0[:, : self.F]
+
+
+class Retirement:
+    """Keeps staged batches alive until the GPU has finished the step that read them: after
+    the step is issued, ``retire(staged)`` records an event on the current stream and holds
+    the batch; held batches are released once their event has completed, and the host waits
+    for the oldest when more than ``depth`` are held (so it never runs further ahead)."""
+
+    def __init__(self, depth: int = 3):
+        import collections
+
+        self.depth = depth
+        self.q = collections.deque()
+        self.wait_s = 0.0  # host time spent waiting for the GPU (so callers can report issue cost)
+
+    def retire(self, staged) -> None:
+        ev = torch.cuda.Event()
+        ev.record()
+        self.q.append((ev, staged))
+        while self.q and self.q[0][0].query():
+            self.q.popleft()
+        if len(self.q) > self.depth:
+            import time
+
+            t0 = time.perf_counter()
+            while len(self.q) > self.depth:
+                ev0, _ = self.q.popleft()
+                ev0.synchronize()
+            self.wait_s += time.perf_counter() - t0
+
+    def drain(self) -> None:
+        while self.q:
+            ev0, _ = self.q.popleft()
+            ev0.synchronize()
 
 
 class PeerExchange:
