@@ -360,7 +360,15 @@ __device__ __forceinline__ int s3_voff(int64_t ld, int r0, int rlim, int t) {
 // swizzled by bit 3 of the row so that every 16-lane group of a ds_read_b128 (lanes
 // {0-3,12-15,20-27}, {4-11,16-19,28-31}, ...: MI355X_MICROARCH.md §LDS) covers all 64 banks
 // (unswizzled, rows r and r + 8 of a group share banks: 2-way conflicts, measured).
-__device__ __forceinline__ int s3_chunk(int row, int h) { return (2 * row + (h ^ ((row >> 3) & 1))) * 8; }
+// k-major sources store one row per lane with a wave-uniform half, so their images are laid
+// out half-major, [h][row]: a ds_write_b128 group of 8 lanes then covers 128 contiguous bytes
+// (the [row][h] image was 2-way: 0.33 of the LDS cycles of the weight-gradient kernels), and
+// each ds_read_b128 group {0-3,12-15,20-27} / {4-11,16-19,28-31} still covers 64 banks.
+template <bool KMAJ>
+__device__ __forceinline__ int s3_chunk(int row, int h) {
+  if constexpr (KMAJ) return (h * BM + row) * 8;
+  else return (2 * row + (h ^ ((row >> 3) & 1))) * 8;
+}
 
 // Split 8 floats into their three bf16 pieces and store them into the stage's images.
 template <bool KMAJ>
@@ -384,17 +392,19 @@ __device__ __forceinline__ void s3_store(unsigned short* __restrict__ S, int t, 
     pm[j] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
     pl[j] = __builtin_amdgcn_perm(__float_as_uint(l.y), __float_as_uint(l.x), 0x07060302u);
   }
-  const int off = s3_chunk(rr, kh);
+  const int off = s3_chunk<KMAJ>(rr, kh);
   *reinterpret_cast<u4v*>(S + off) = ph;
   *reinterpret_cast<u4v*>(S + S3_PIECE + off) = pm;
   *reinterpret_cast<u4v*>(S + 2 * S3_PIECE + off) = pl;
 }
 
+template <bool KMAJ>
 __device__ __forceinline__ bf8v s3_frag(const unsigned short* __restrict__ S, int piece, int row, int h) {
-  return __builtin_bit_cast(bf8v, *reinterpret_cast<const u4v*>(S + piece * S3_PIECE + s3_chunk(row, h)));
+  return __builtin_bit_cast(bf8v, *reinterpret_cast<const u4v*>(S + piece * S3_PIECE + s3_chunk<KMAJ>(row, h)));
 }
 
 // The six piece products of one k16 step into the wave's 2 x 2 accumulators (small terms first).
+template <bool AK, bool BKM>
 __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, const unsigned short* __restrict__ Sb,
                                        int ra0, int rb0, int li, int lh, f16v acc[2][2]) {
   bf8v a[2][3], bb[2][3];
@@ -402,8 +412,8 @@ __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, co
   for (int p = 0; p < 3; ++p)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      a[i][p] = s3_frag(Sa, p, ra0 + i * 32 + li, lh);
-      bb[i][p] = s3_frag(Sb, p, rb0 + i * 32 + li, lh);
+      a[i][p] = s3_frag<AK>(Sa, p, ra0 + i * 32 + li, lh);
+      bb[i][p] = s3_frag<BKM>(Sb, p, rb0 + i * 32 + li, lh);
     }
   constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
   constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
@@ -485,17 +495,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     for (; kt + 1 < nfull; kt += 2) {
       // tile kt from stage 0; tile kt+1 (set 1) -> stage 1; set 0 <- tile kt+2
       load_ab(kt + 2, ra[0], rb[0]);
-      s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      s3_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
       store_ab(1, ra[1], rb[1]);
       __syncthreads();
       // tile kt+1 from stage 1; tile kt+2 (set 0) -> stage 0; set 1 <- tile kt+3
       load_ab(kt + 3, ra[1], rb[1]);
-      s3_mma(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
+      s3_mma<AK, BKM>(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
       store_ab(0, ra[0], rb[0]);
       __syncthreads();
     }
     if (nfull & 1) {  // odd count: the last full tile is in stage 0
-      s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      s3_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
       __syncthreads();
     }
   }
@@ -505,7 +515,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, rb[0]);
     store_ab(0, ra[0], rb[0]);
     __syncthreads();
-    s3_mma(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+    s3_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
   }
 
   float* __restrict__ Cb;
