@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--e2e-steps", type=int, default=60, help="steps of the live-sampling end-to-end run")
     ap.add_argument("--no-e2e", action="store_true", help="skip the live-sampling end-to-end run")
     ap.add_argument("--workers", type=int, default=0, help="sampler threads per rank (0: auto)")
+    ap.add_argument("--compute-priority", default="high", choices=["high", "normal"],
+                    help="priority of the stream the training step runs on (the staging stream stays normal)")
     ap.add_argument("--staging", default="copy", choices=["copy", "zerocopy"],
                     help="non-buffered feature rows: host gather into pinned memory + one hipMemcpyAsync "
                          "(copy), or the GPU reads the mapped host table over PCIe (zerocopy: measured "
@@ -339,7 +341,22 @@ def main():
     nb = len(dbatches)
     retire = staging.Retirement()
 
+    # The step runs on a high-priority stream: the staging stream's gathers and operand builds
+    # for the next batch (default priority) then fill the compute stream's gaps instead of
+    # taking CU slots from the layer-0 aggregation they overlap (--compute-priority normal: off).
+    lo_pri, hi_pri = torch.cuda.Stream.priority_range()
+    compute_stream = torch.cuda.Stream(device=dev, priority=hi_pri) if args.compute_priority == "high" else None
+
     def pipeline(next_item, steps):
+        if compute_stream is None:
+            return _pipeline(next_item, steps)
+        compute_stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(compute_stream):
+            loss = _pipeline(next_item, steps)
+        torch.cuda.current_stream(dev).wait_stream(compute_stream)
+        return loss
+
+    def _pipeline(next_item, steps):
         """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
         needed + the operand builds). Batch i+1's X0 staging and batch_fn run on the side
         stream, issued before batch i's step, so they overlap that step's kernels."""
