@@ -29,8 +29,14 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
     if (e_ != hipSuccess) return ::gnn::fail((int)e_, "%s launch: %s", name, hipGetErrorString(e_)); \
   } while (0)
 
+// A failed runtime call is reported by status code and also cleared from HIP's per-thread
+// last-error slot: the caller gets the RuntimeError once, and later unrelated calls (torch's
+// own error checks) do not pick up the stale error.
 #define GNN_HIP(call, name)                                                                \
   do {                                                                                     \
     hipError_t e_ = (call);                                                                \
-    if (e_ != hipSuccess) return ::gnn::fail((int)e_, "%s: %s", name, hipGetErrorString(e_)); \
+    if (e_ != hipSuccess) {                                                                \
+      (void)hipGetLastError();                                                             \
+      return ::gnn::fail((int)e_, "%s: %s", name, hipGetErrorString(e_));                  \
+    }                                                                                      \
   } while (0)

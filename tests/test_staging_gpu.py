@@ -97,3 +97,49 @@ def test_zero_copy_gather_rejects_unregistered_memory(dev):
     dst = torch.empty(4, 8, device=dev)
     with pytest.raises(RuntimeError, match="hipHostGetDevicePointer"):
         cso.gather_rows_host(host, idx, dst, None)
+
+
+def test_retirement_pipeline_on_priority_stream_matches(dev):
+    # bench.py's pipeline: batch i+1 staged on the side stream before batch i's step, the step
+    # on a high-priority stream, staged buffers kept alive by one retirement event per step
+    # (depth 1: the host waits for the GPU every step, so freed blocks are reused at once)
+    # instead of record_stream — same losses and weights as the record_stream path.
+    lap, labels, train = _setup(seed=7)
+    N = lap.shape[0]
+    pl = placement.create_buffer_ours(lap, train, 500, [0], 3, alpha=0)
+    feats = torch.randn(N, 30)
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    ld = loader.BatchLoader(lap, labels, train, 800, 128, [1, 1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], rank=0, world_size=1, store=store, workers=2,
+                            seed=3)
+    lbs = list(ld.epoch(1))[:6]
+    ld.close()
+
+    def run(retire, stream):
+        torch.manual_seed(0)
+        m = build_model("graphsage", 30, 16, [1, 1, 1], 7, dropout=0.0, fused=True).to(dev)
+        tr = Trainer(m, 0.01, dev)
+        stager = staging.Stager(store)
+        losses = []
+        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            it = iter(lbs)
+            nxt = lambda lb: stager.issue(lb.plan, lambda: lb.host.to_device(dev, with_coo=False))
+            staged = nxt(next(it))
+            for i in range(len(lbs)):
+                staged_next = nxt(next(it)) if i + 1 < len(lbs) else None
+                x0 = staged.wait(retire)
+                db = staged.batch
+                losses.append(tr.step(x0, staged.adjs, db.sampled_nodes, db.labels))
+                if retire is not None:
+                    retire.retire(staged)
+                staged = staged_next
+        torch.cuda.synchronize()
+        return [float(l) for l in losses], [p.detach().clone() for p in m.parameters()]
+
+    lo, hi = torch.cuda.Stream.priority_range()
+    ref_l, ref_p = run(None, torch.cuda.Stream(device=dev))
+    got_l, got_p = run(staging.Retirement(depth=1), torch.cuda.Stream(device=dev, priority=hi))
+    assert got_l == ref_l
+    for a, b in zip(got_p, ref_p):
+        assert torch.equal(a, b)
