@@ -1,13 +1,24 @@
 """Benchmark: Reddit GraphSAGE / LADIES mini-batch training on MI355X (BASELINE.json config 2).
 
-One step = one data-parallel mini-batch training iteration of the reference's hot path
-(main.py:122-170) on a pre-sampled LADIES batch whose operands and index arrays are resident
-in HBM: X0 staging (own-GPU buffer gather + pinned-host rows H2D on a side stream, peer rows
-by RCCL all-to-all when N > 1), 3 HIP aggregation forwards + 2 backwards inside GraphSAGE
-(samp_num 8192, batch 512, nhid 512, orders 1,1,1, F = 602, 41 classes), loss, backward,
-clip_grad_norm_(5), RCCL all-reduce(SUM) of the flat gradient, Adam.
+Headline `value` = END-TO-END mini-batches/s, as the reference's training loop runs
+(main.py:115-170): every timed step takes a batch LIVE from the sampler pool (the native
+LADIES sampler + the host gather of the non-buffered feature rows, in worker threads; the
+reference's prepare_data thread pool, sampler.py:163-193), stages X0 (own-GPU buffer gather,
+pinned host rows H2D on a side stream, peer rows by RCCL all-to-all when N > 1, the per-step
+peer negotiation included), builds the operands, and runs 3 HIP aggregation forwards + 2
+backwards inside GraphSAGE (samp_num 8192, batch 512, nhid 512, orders 1,1,1, F = 602, 41
+classes), loss, backward, clip_grad_norm_(5), RCCL all-reduce(SUM) of the flat gradient, Adam.
+The warm-up drains the sampler's prefetch queue first, so the timed steps run in steady
+state (nothing pre-sampled is consumed inside the timed region).
+
+Second figure `gpu_step`: the same step over DISTINCT pre-sampled batches (one per timed
+step, none cycled) whose CSR pieces are resident in HBM — the GPU side alone. The SpMM
+roofline comes from that run (HIP events on the launch stream around every aggregation).
+
 Synthetic Reddit-shaped graph: Chung-Lu lognormal sigma 1.3, N = 232,965,
 ~23.1 M nnz, N(0,1) fp32 features (StandardScaler'd analogue), buffer_size = 0.1.
+`--cpu`: BASELINE config 1 (samp 512, batch 128, one process on the CPU through the product's
+torch.sparse.mm device branch).
 
 Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
 Rank 0 prints ONE JSON line.
@@ -31,7 +42,11 @@ from gnn_amd import graphs, placement, sampler, staging  # noqa: E402
 from gnn_amd.models import build_model  # noqa: E402
 from gnn_amd.train import Trainer, init_distributed  # noqa: E402
 
+METRIC = "mini-batches/sec + SpMM HBM GB/s, Reddit GraphSAGE/LADIES at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+# Row gathers served by an XCD's L2 (MI355X_MICROARCH.md §Indexed rows: 66-73 GB/s per CU,
+# 16.8-18.8 TB/s chip-wide): the ceiling of a gather whose table is re-read from cache.
+L2_GATHER_PEAK_GBS = 18800.0
 
 
 def log(*a):
@@ -40,6 +55,8 @@ def log(*a):
 
 
 GRAPH_NAMES = {"reddit": "Reddit", "products": "ogbn-products", "papers": "ogbn-papers100M-scaled", "tiny": "tiny"}
+SAMPLERS = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
+            "fastgcn": sampler.fastgcn_sample_host}
 
 
 def parse():
@@ -47,24 +64,23 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batches", type=int, default=4, help="distinct pre-sampled batches per rank (cycled)")
     ap.add_argument("--model", default="graphsage", choices=["graphsage", "gcn"])
     ap.add_argument("--sampler", default="ladies", choices=["ladies", "subgraph", "fastgcn"])
-    ap.add_argument("--samp-num", type=int, default=8192)
-    ap.add_argument("--batch-size", type=int, default=512)
+    ap.add_argument("--samp-num", type=int, default=None, help="default 8192 (512 with --cpu)")
+    ap.add_argument("--batch-size", type=int, default=None, help="default 512 (128 with --cpu)")
     ap.add_argument("--nhid", type=int, default=512)
     ap.add_argument("--buffer-size", type=float, default=0.1)
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--graph", default="reddit", choices=["reddit", "products", "papers", "tiny"],
                     help="synthetic graph shape: reddit (configs 1-2), products (configs 3, 5), papers "
                          "(config 4's per-batch geometry on a graph scaled to the box), tiny (smoke)")
+    ap.add_argument("--cpu", action="store_true", help="BASELINE config 1: one process on the CPU (no GPU)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic child run")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC traffic child runs")
+    ap.add_argument("--no-gpu-step", action="store_true", help="skip the distinct-batch GPU-step run")
     ap.add_argument("--unfused", action="store_true", help="torch elementwise layer tail instead of the HIP one")
-    ap.add_argument("--e2e-steps", type=int, default=60, help="steps of the live-sampling end-to-end run")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the live-sampling end-to-end run")
     ap.add_argument("--workers", type=int, default=0, help="sampler threads per rank (0: auto)")
     ap.add_argument("--compute-priority", default="high", choices=["high", "normal"],
                     help="priority of the stream the training step runs on (the staging stream stays normal)")
@@ -72,33 +88,23 @@ def parse():
                     help="non-buffered feature rows: host gather into pinned memory + one hipMemcpyAsync "
                          "(copy), or the GPU reads the mapped host table over PCIe (zerocopy: measured "
                          "slower, it slows the concurrent compute kernels)")
-    ap.add_argument("--cprofile", default="", help="after the timed run, cProfile 20 steps into this text file")
-    ap.add_argument("--torch-profile", default="", help="after the timed run, write a torch.profiler op table here")
+    ap.add_argument("--cprofile", default="", help="after the timed runs, cProfile 20 GPU steps into this file")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.samp_num is None:
+        a.samp_num = 512 if a.cpu else 8192
+    if a.batch_size is None:
+        a.batch_size = 128 if a.cpu else 512
+    return a
 
 
-def sample_batches(args, lap, labels, train, pl, rank, world):
-    batches = sampler.rank_batches(train, args.batch_size, rank, world, iter_num=1)[: args.batches]
-    rs = np.random.RandomState(1234 + rank)
-    seeds = rs.randint(2**31 - 1, size=len(batches))
-    out = []
-    fn = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
-          "fastgcn": sampler.fastgcn_sample_host}[args.sampler]
-    for s, b in zip(seeds, batches):
-        out.append(fn(int(s), b, np.array([args.samp_num] * 5), lap.shape[0], lap, labels,
-                                              [1, 1, 1], pl.device_id_of_nodes_group[rank],
-                                              pl.idx_of_nodes_on_device_group[rank], None, 1.0, list(range(world))))
-    return out
-
-
+# ----------------------------------------------------------------------------- PMC traffic
 def _counter_rows(d):
     import csv
     import glob
 
-    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     rows = []
-    for f in files:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             rows.extend(csv.DictReader(fh))
     return rows
@@ -119,13 +125,21 @@ def _kernel_symbol(name: str) -> str:
     return name.strip()
 
 
+def _dump_batch(hb, path):
+    np.savez(path, **{f"l{i}_{k}": getattr(L, k) for i, L in enumerate(hb.layers)
+                      for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
+             **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(hb.layers)})
+
+
 def pmc_traffic(hb, F, hidden, workdir="/tmp/gnn_bench_pmc"):
-    """Bytes per launch leaving L2 (toward the Infinity Cache / HBM) for each aggregation
-    kernel instantiation, from rocprofv3 PMC counters (FETCH_SIZE and WRITE_SIZE in separate
-    passes) over the forward calls of batch 0 laid out as the benchmark runs them, each
-    counter corrected by a calibration gather of known bytes with the same 16-byte row
-    vectors (MI355X_MICROARCH.md §HBM). Runs the probe as a CHILD process before this process
-    has touched the GPU. Returns {"by_kernel": {symbol: {...}}, corrections}, or None."""
+    """Per-launch bytes leaving L2 (toward the Infinity Cache / HBM) and the L2 hit rate of
+    each aggregation kernel instantiation, from rocprofv3 PMC counters in three passes
+    (FETCH_SIZE; WRITE_SIZE; TCC_HIT_sum + TCC_MISS_sum) over scripts/pmc_probe.py: batch 0's
+    forward calls laid out as the benchmark runs them. FETCH_SIZE / WRITE_SIZE are corrected
+    by a calibration launch of the SAME kernel instantiation (4 rows x 256 B per wave
+    instruction) over an operand whose every X row is gathered once from a 2.4 GB table, so
+    its bytes are known (MI355X_MICROARCH.md §HBM: calibrate in your own access pattern).
+    Runs the probe as CHILD processes before this process has touched the GPU."""
     import shutil
     import subprocess
 
@@ -133,49 +147,57 @@ def pmc_traffic(hb, F, hidden, workdir="/tmp/gnn_bench_pmc"):
         return None
     os.makedirs(workdir, exist_ok=True)
     npz = os.path.join(workdir, "batch0.npz")
-    L0 = hb.layers
-    np.savez(npz, **{f"l{i}_{k}": getattr(L, k) for i, L in enumerate(L0)
-                     for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
-             **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
+    _dump_batch(hb, npz)
     probe = os.path.join(REPO, "scripts", "pmc_probe.py")
-    calib, kern = {}, {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(workdir, counter)
+    calib, kern, info = {}, {}, None
+    for counters in (["FETCH_SIZE"], ["WRITE_SIZE"], ["TCC_HIT_sum", "TCC_MISS_sum"]):
+        d = os.path.join(workdir, counters[0])
         shutil.rmtree(d, ignore_errors=True)
-        cmd = ["rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
+        cmd = ["rocprofv3", "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "p", "--",
                sys.executable, probe, npz, "--feat", str(F), "--hidden", str(hidden)]
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
-            log(f"pmc pass {counter} failed rc={r.returncode}: {r.stderr[-500:]}")
+            log(f"pmc pass {counters} failed rc={r.returncode}: {r.stderr[-500:]}")
             return None
-        cal = []
-        for row in _counter_rows(d):
-            if row.get("Counter_Name") != counter:
+        for line in r.stdout.splitlines():
+            if line.startswith("PMCPROBE "):
+                info = json.loads(line[len("PMCPROBE "):])
+        rows = sorted(_counter_rows(d), key=lambda row: int(row.get("Dispatch_Id", 0)))
+        first_build = min((int(row["Dispatch_Id"]) for row in rows if "build_operand" in row.get("Kernel_Name", "")),
+                          default=None)
+        for row in rows:
+            name, cn = row.get("Kernel_Name", ""), row.get("Counter_Name")
+            if "spmm_unit_kernel" not in name or cn not in counters:
                 continue
-            name, v = row.get("Kernel_Name", ""), float(row.get("Counter_Value", "nan"))
-            if "gather_rows_kernel" in name:
-                cal.append(v)
-            elif "spmm_unit_kernel" in name:
-                kern.setdefault(_kernel_symbol(name), {}).setdefault(counter, []).append(v)
-        if not cal:
-            return None
-        calib[counter] = float(np.median(cal))
-    ld = (F + 3) // 4 * 4
-    n = int(1.2e9 // (ld * 4))
-    known = n * ld * 4  # bytes read (and written) by one calibration gather
-    read_corr = known / (calib["FETCH_SIZE"] * 1024.0)
-    write_corr = known / (calib["WRITE_SIZE"] * 1024.0)
+            v = float(row.get("Counter_Value", "nan"))
+            if first_build is not None and int(row["Dispatch_Id"]) < first_build:
+                calib.setdefault(cn, []).append(v)  # the calibration launches come first
+            else:
+                kern.setdefault(_kernel_symbol(name), {}).setdefault(cn, []).append(v)
+    if info is None or "FETCH_SIZE" not in calib or "WRITE_SIZE" not in calib:
+        return None
+    read_corr = info["calib_known_read_bytes"] / (float(np.median(calib["FETCH_SIZE"])) * 1024.0)
+    write_corr = info["calib_known_write_bytes"] / (float(np.median(calib["WRITE_SIZE"])) * 1024.0)
     by = {}
     for sym, c in kern.items():
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             continue
         rd = float(np.mean(c["FETCH_SIZE"])) * 1024.0 * read_corr
         wr = float(np.mean(c["WRITE_SIZE"])) * 1024.0 * write_corr
-        by[sym] = {"bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
-                   "launches": len(c["FETCH_SIZE"])}
-    return {"by_kernel": by, "read_correction": round(read_corr, 4), "write_correction": round(write_corr, 4)}
+        e = {"bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr, "launches": len(c["FETCH_SIZE"])}
+        if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+            h, m = float(np.sum(c["TCC_HIT_sum"])), float(np.sum(c["TCC_MISS_sum"]))
+            e["l2_hit_rate"] = round(h / (h + m), 4) if h + m > 0 else None
+        by[sym] = e
+    out = {"by_kernel": by, "read_correction": round(read_corr, 4), "write_correction": round(write_corr, 4),
+           "calibration": {k: info[k] for k in ("calib_known_read_bytes", "calib_known_write_bytes", "calib_tiles")}}
+    if "TCC_HIT_sum" in calib and "TCC_MISS_sum" in calib:
+        h, m = float(np.sum(calib["TCC_HIT_sum"])), float(np.sum(calib["TCC_MISS_sum"]))
+        out["calibration"]["l2_hit_rate"] = round(h / (h + m), 4) if h + m > 0 else None
+    return out
 
 
+# ----------------------------------------------------------------------------- CPU legs
 def cpu_baseline(args, hb, feats, num_classes):
     """Reference CPU path (torch.sparse.mm) full training step on the same batch, rank 0 / N=1."""
     from oracle.cpu_reference import cpu_inputs, cpu_train_step, torch_spmm
@@ -237,108 +259,188 @@ def default_workers(world: int) -> int:
     return max(2, min(14, cpu_budget() // max(world, 1) - 2))
 
 
-def end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev):
-    """Mini-batches/s with sampling in the loop: the native LADIES sampler + host-row staging
-    in worker threads (gnn_amd.loader.BatchLoader) feeding the same training step. Also the
-    single-thread sampler cost per batch, native and numpy (rank 0)."""
+def workload_name(args, spec) -> str:
+    model = "GraphSAGE" if args.model == "graphsage" else "GCN"
+    smp = args.sampler.upper() if args.sampler != "fastgcn" else "FastGCN"
+    w = f"{GRAPH_NAMES[args.graph]} {model} {smp} samp_num={args.samp_num} batch_size={args.batch_size}"
+    if args.graph == "reddit" and (args.model, args.sampler) == ("graphsage", "ladies"):
+        if (args.samp_num, args.batch_size) == (8192, 512) and not args.cpu:
+            w += " (BASELINE config 2)"
+        if (args.samp_num, args.batch_size) == (512, 128) and args.cpu:
+            w += " (BASELINE config 1, CPU)"
+    return w
+
+
+def run_cpu(args, spec, A, lap, labels, feats, num_classes, train):
+    """BASELINE config 1: one process on the CPU, the product's torch.sparse.mm device branch
+    (gnn_amd.custom_sparse_ops), native LADIES sampling in the loader's worker threads."""
     from gnn_amd.loader import BatchLoader
 
-    workers = args.workers or default_workers(world)
-    ld = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pl.device_id_of_nodes_group[rank],
-                     pl.idx_of_nodes_on_device_group[rank], rank=rank, world_size=world, store=store,
-                     workers=workers, seed=4242, kind=args.sampler)
+    N = A.shape[0]
+    pl = placement.create_buffer(lap, train, int(args.buffer_size * N), [0], 3, alpha=0)
+    torch.manual_seed(0)
+    model = build_model(args.model, feats.shape[1], args.nhid, [1, 1, 1], num_classes, 0.1)
+    trainer = Trainer(model, args.lr, "cpu")
+    workers = args.workers or max(1, min(4, cpu_budget() // 4))
+    ld = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pl.device_id_of_nodes_group[0],
+                     pl.idx_of_nodes_on_device_group[0], workers=workers, seed=4242, kind=args.sampler)
     it = ld.forever()
 
-    def nxt():
-        lb = next(it)
-        return lb.plan, lambda: lb.host.to_device(dev, with_coo=False)
+    def step():
+        adjs, x0, sampled, y = next(it).host.cpu_inputs(feats)
+        return trainer.step(x0, adjs, sampled, y)
 
-    warm = max(2 * workers, 10)
-    pipeline(nxt, warm)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
     t0 = time.perf_counter()
-    pipeline(nxt, args.e2e_steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    for _ in range(args.steps):
+        loss = step()
     el = time.perf_counter() - t0
     ld.close()
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
-    out = {"value": round(world * args.e2e_steps / el, 3), "unit": "mini-batches/s", "steps": args.e2e_steps,
-           "sampler_workers_per_rank": workers,
-           "what": f"live {args.sampler} sampling (native, worker threads) + pinned host staging + H2D + the same step"}
-    if rank == 0:
-        chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
-        fn = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_sample_host,
-              "fastgcn": sampler.fastgcn_sample_host}[args.sampler]
-        sm = np.array([args.samp_num] * 5)
-        pdev, pidx = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
-        t = time.perf_counter()
-        for i, c in enumerate(chunks[:3]):
-            fn(i, c, sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)))
-        nat = (time.perf_counter() - t) / 3
-        t = time.perf_counter()
-        fn(3, chunks[3], sm, lap.shape[0], lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)),
-           native=False)
-        npy = time.perf_counter() - t
-        out["sampler_ms_per_batch_1thread"] = {"native": round(nat * 1e3, 1), "numpy": round(npy * 1e3, 1)}
-    return out
+    line = {"metric": METRIC, "value": round(args.steps / el, 3), "unit": "mini-batches/s", "n_gpus": 0,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic (Chung-Lu {spec.name}-shaped graph, N(0,1) features, random-init model); live "
+                    f"{args.sampler} sampling in {workers} worker threads",
+            "config": {"workload": workload_name(args, spec), "device": "cpu", "torch_threads": torch.get_num_threads(),
+                       "cpu_budget": cpu_budget(), "model": args.model, "global_batch": args.batch_size,
+                       "samp_num": args.samp_num, "nhid": args.nhid, "feat_dim": int(feats.shape[1]),
+                       "num_nodes": int(N), "parallelism": "none (one process)"},
+            "roofline": None, "cpu_baseline": None, "final_loss": round(float(loss), 5)}
+    print(json.dumps(line), flush=True)
 
 
+# ----------------------------------------------------------------------------- roofline
+def roofline_from(recs, step_batches, args, traffic, steps):
+    """Per call site and for the dominant aggregation kernel: algorithmic, compulsory and
+    (PMC) L2-egress byte rates over the HIP-event launch durations of the distinct-batch run.
+    Call sites per step, in call order: 3 forwards, then the backwards of layers 2 and 1."""
+    names = ["fwd_L0", "fwd_L1", "fwd_L2", "bwd_L2", "bwd_L1"]
+    site, kname = {}, {}
+    uniq_cache = {}
+    for i, (tag, ms, nbytes, kn, dims) in enumerate(recs):
+        key = names[i % len(names)]
+        assert key.startswith(tag), (key, tag)
+        hb = step_batches[(i // len(names)) % len(step_batches)]
+        li = int(key[-1])
+        L = hb.layers[li]
+        ck = (id(hb), key)
+        if ck not in uniq_cache:  # distinct X rows the call gathers (cols of A, or non-empty rows for Aᵀ)
+            uniq_cache[ck] = (np.unique(L.colidx).size if key.startswith("fwd")
+                              else int(np.count_nonzero(np.diff(L.rowptr))))
+        F, M, nnz = dims["F"], dims["M"], dims["nnz"]
+        comp = uniq_cache[ck] * F * 4 + nnz * 8 + (M + 1) * 4 + M * F * 4 + dims["res_rows"] * F * 4
+        if dims["res_rows"]:
+            comp += M * 4
+        e = site.setdefault(key, [0.0, 0, 0, 0])
+        e[0] += ms
+        e[1] += nbytes
+        e[2] += 1
+        e[3] += comp
+        kname[key] = kn
+    detail = {k: {"avg_us": round(1e3 * ms / n, 2), "GB_per_launch": round(nb / n / 1e9, 4),
+                  "alg_GBps": round(nb / (ms * 1e-3) / 1e9, 1),
+                  "compulsory_GB_per_launch": round(cb / n / 1e9, 4),
+                  "compulsory_GBps": round(cb / (ms * 1e-3) / 1e9, 1), "kernel": kname[k]}
+              for k, (ms, nb, n, cb) in site.items()}
+    byk = {}
+    for key, (ms_, nb_, n_, cb_) in site.items():
+        e = byk.setdefault(kname[key], [0.0, 0, 0, 0, []])
+        e[0] += ms_
+        e[1] += nb_
+        e[2] += n_
+        e[3] += cb_
+        e[4].append(key)
+    dom = max(byk, key=lambda k_: byk[k_][0])
+    ms, nbytes, n, cbytes, sites = byk[dom]
+    t = ms * 1e-3 / n  # average launch duration, s
+    alg = nbytes / n
+    comp = cbytes / n
+    tr = (traffic or {}).get("by_kernel", {}).get(dom)
+    roof = {"bound": "hbm"}
+    if tr:
+        # the bytes that left L2 for the Infinity Cache / HBM (calibrated PMC), per launch
+        egress = tr["bytes_per_launch"]
+        roof.update({"achieved": round(egress / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(egress / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": round(egress / 1e9, 4),
+                     "basis": "PMC L2-egress bytes per launch (FETCH_SIZE + WRITE_SIZE, calibrated) / HIP-event "
+                              "launch duration"})
+    else:
+        roof.update({"achieved": round(comp / t / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(comp / t / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "basis": "compulsory bytes per launch / HIP-event launch duration (no PMC pass in this run)"})
+    roof.update({
+        "kernel": f"{dom} (call sites {' + '.join(sorted(sites))}), avg {1e6 * t:.1f} us/launch over {n} launches",
+        "avg_us": round(1e6 * t, 2),
+        "compulsory": {"GB_per_launch": round(comp / 1e9, 4), "GBps": round(comp / t / 1e9, 1),
+                       "frac_of_hbm_peak": round(comp / t / 1e9 / HBM_PEAK_GBS, 4),
+                       "what": "distinct X rows gathered x F x 4 + (col, val) + rowptr + Y (+ residual rows)"},
+        "algorithmic": {"GB_per_launch": round(alg / 1e9, 4), "GBps": round(alg / t / 1e9, 1),
+                        "what": "SURVEY.md §8(d): every gathered X row counted (re-reads served by L2 / Infinity "
+                                "Cache), no fraction: it is not an HBM quantity"},
+        "l2_gather": {"ceiling_GBps": L2_GATHER_PEAK_GBS, "frac": round(alg / t / 1e9 / L2_GATHER_PEAK_GBS, 4),
+                      "what": "algorithmic gather rate / the L2-served row-gather rate of MI355X_MICROARCH.md "
+                              "§Indexed rows (18.8 TB/s chip-wide)"},
+    })
+    if tr:
+        roof["l2_hit_rate"] = tr.get("l2_hit_rate")
+        roof["egress_over_compulsory"] = round(tr["bytes_per_launch"] / comp, 2)
+        roof["pmc"] = {"read_correction": traffic["read_correction"], "write_correction": traffic["write_correction"],
+                       "calibration": traffic["calibration"],
+                       "all_kernels_GB_per_launch": {k: round(v["bytes_per_launch"] / 1e9, 4)
+                                                     for k, v in traffic["by_kernel"].items()},
+                       "all_kernels_l2_hit_rate": {k: v.get("l2_hit_rate") for k, v in traffic["by_kernel"].items()}}
+    tot_ms = sum(v[0] for v in site.values())
+    tot_b = sum(v[1] for v in site.values())
+    roof["all_spmm_alg_GBps"] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)
+    roof["spmm_ms_per_step"] = round(tot_ms / steps, 3)
+    return roof, detail
+
+
+# ----------------------------------------------------------------------------- main
 def main():
     args = parse()
+    spec = {"reddit": graphs.REDDIT, "products": graphs.PRODUCTS, "papers": graphs.PAPERS_SCALED,
+            "tiny": graphs.TINY}[args.graph]
+    t0 = time.time()
+    A, labels, feats, num_classes, train, valid, test = graphs.make_dataset(spec, seed=0)
+    lap = graphs.lap_matrix(A, args.model)
+    N = A.shape[0]
+    log(f"graph {spec.name}: N={N} nnz={A.nnz} ({time.time() - t0:.1f}s)")
+    if args.cpu:
+        return run_cpu(args, spec, A, lap, labels, feats, num_classes, train)
+
     rank, world, local = init_distributed()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     dev = torch.device("cuda", local)
-
-    t0 = time.time()
-    spec = {"reddit": graphs.REDDIT, "products": graphs.PRODUCTS, "papers": graphs.PAPERS_SCALED,
-            "tiny": graphs.TINY}[args.graph]
-    A, labels, feats, num_classes, train, valid, test = graphs.make_dataset(spec, seed=0)
-    lap = graphs.row_normalize(A)
-    lap.sum_duplicates()
-    N = A.shape[0]
-    log(f"graph {spec.name}: N={N} nnz={A.nnz} ({time.time() - t0:.1f}s)")
     k = int(args.buffer_size * N)
     pl = placement.create_buffer(lap, train, k, list(range(world)), 3, alpha=0)
+    pdev, pidx = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
     log(f"placement k={k} per GPU ({time.time() - t0:.1f}s)")
-    host_batches = sample_batches(args, lap, labels, train, pl, rank, world)
-    log(f"sampled {len(host_batches)} batches ({time.time() - t0:.1f}s); nnz/batch={host_batches[0].nnz()}")
+    samp = np.array([args.samp_num] * 5)
+    fn = SAMPLERS[args.sampler]
+    probe_batch = fn(99, sampler.rank_batches(train, args.batch_size, rank, world, 0)[0], samp, N, lap, labels,
+                     [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)))
     traffic = None
-    if rank == 0 and world == 1 and not args.no_traffic:
-        # before this process initialises the GPU: the probe is a child process
+    if rank == 0 and world == 1 and not args.no_traffic and not args.no_roofline:
+        # before this process initialises the GPU: the probes are child processes
         try:
-            traffic = pmc_traffic(host_batches[0], feats.shape[1], 2 * args.nhid)
+            traffic = pmc_traffic(probe_batch, feats.shape[1], 2 * args.nhid if args.model == "graphsage" else args.nhid)
         except Exception as e:  # profiler trouble must not sink the benchmark
             log(f"pmc traffic measurement skipped: {e!r}")
         log(f"pmc traffic done ({time.time() - t0:.1f}s): {traffic}")
+    if args.dump_batch and rank == 0:
+        _dump_batch(probe_batch, args.dump_batch)
     torch.cuda.set_device(dev)
 
     store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank, zero_copy=args.staging == "zerocopy")
     exchange = staging.PeerExchange() if world > 1 else None
     stager = staging.Stager(store, exchange)
-    plans = [staging.make_plan(hb, store, rank, world) for hb in host_batches]
-    # CSR pieces, labels and sampled_nodes resident in HBM; the operand builder (the
-    # create_coo_tensor kernel) runs for every step, on the staging stream ahead of it.
-    dbatches = [hb.to_device(dev, build=False) for hb in host_batches]
-    if args.dump_batch and rank == 0:
-        L0 = host_batches[0].layers
-        np.savez(args.dump_batch, **{f"l{i}_{k}": getattr(L, k) for i, L in enumerate(L0)
-                                     for k in ("fullrowptr", "rowptr", "colidx", "normfact")},
-                 **{f"l{i}_shape": np.array(L.shape) for i, L in enumerate(L0)})
-
     torch.manual_seed(0)
     model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
     trainer = Trainer(model, args.lr, dev)
     torch.cuda.synchronize()
     log(f"setup done ({time.time() - t0:.1f}s); params={trainer.num_params}")
-
-    nb = len(dbatches)
     retire = staging.Retirement()
 
     # The step runs on a high-priority stream: the staging stream's gathers and operand builds
@@ -371,173 +473,147 @@ def main():
             staged = staged_next
         return loss
 
-    def run(steps, start):
-        """Pre-sampled batches, operands resident in HBM, cycled (the headline step)."""
-        k = [start]
-
-        def nxt():
-            j = k[0] % nb
-            k[0] += 1
-            db = dbatches[j]
-            return plans[j], lambda: (db.build_operands(), db)[1]
-        return pipeline(nxt, steps)
-
-    run(args.warmup, 0)
-    cso.enable_timing(not args.no_roofline)
-    stager.timing = []
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    retire.wait_s = 0.0
-    t_start = time.perf_counter()
-    loss = run(args.steps, args.warmup)
-    # host time to issue the steps, without the waits that keep it <= 3 steps ahead of the GPU
-    t_issued = time.perf_counter() - retire.wait_s
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t_start
-    cso.enable_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-    recs = cso.take_timing_records()
-    h_bytes, h_sec = stager.take_timing()
-    staging_info = {"mode": args.staging, "host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
-                    "h2d_GBps": round(h_bytes / h_sec / 1e9, 1) if h_sec > 0 else None,
-                    "h2d_ms_per_batch": round(1e3 * h_sec / args.steps, 3),
-                    "note": ("GPU gather of the host rows from the pinned, device-mapped feature table over PCIe"
-                             if args.staging == "zerocopy" else
-                             "host rows gathered into pinned memory by the producer, one hipMemcpyAsync")
-                            + " on the staging stream, overlapped with the previous step"}
-
-    # ------------------------------------------------- end to end, live sampling
-    e2e = None
-    if not args.no_e2e and args.e2e_steps > 0:
-        e2e = end_to_end(args, pipeline, lap, labels, train, pl, store, rank, world, dev)
-    if args.cprofile and rank == 0:
-        import cProfile
-        import pstats
-
-        pr = cProfile.Profile()
-        pr.enable()
-        run(20, 0)
+    def timed(fn_):
+        """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds)."""
+        if world > 1:
+            torch.distributed.barrier()
         torch.cuda.synchronize()
-        pr.disable()
-        with open(args.cprofile, "w") as fh:
-            st = pstats.Stats(pr, stream=fh)
-            st.sort_stats("tottime").print_stats(45)
-            st.sort_stats("cumulative").print_stats(45)
-    if args.torch_profile and rank == 0:
-        from torch.profiler import ProfilerActivity, profile
+        retire.wait_s = 0.0
+        ts = time.perf_counter()
+        out = fn_()
+        issued = time.perf_counter() - ts - retire.wait_s
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        return el, issued, out
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
-            run(3, 0)
+    # ------------------------------------------------- headline: end to end, live sampling
+    from gnn_amd.loader import BatchLoader
+
+    workers = args.workers or default_workers(world)
+    loader = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank,
+                         world_size=world, store=store, workers=workers, seed=4242, kind=args.sampler)
+    it = loader.forever()
+
+    def nxt_live():
+        lb = next(it)
+        return lb.plan, lambda: lb.host.to_device(dev, with_coo=False)
+
+    # warm-up: at least the prefetch queue's depth, so the timed steps start in steady state
+    # (the queue filled during setup holds pre-sampled batches that must not be timed)
+    warm = max(args.warmup, loader.prefetch + 2)
+    pipeline(nxt_live, warm)
+    e2e_s, e2e_issue, loss = timed(lambda: pipeline(nxt_live, args.steps))
+    log(f"end to end: {world * args.steps / e2e_s:.1f} mini-batches/s ({time.time() - t0:.1f}s)")
+
+    # ------------------------------------------------- GPU step over distinct pre-sampled batches
+    gpu_step, roof, spmm_detail, staging_info = None, None, {}, None
+    step_batches = []
+    if not args.no_gpu_step:
+        nwarm = max(2, min(args.warmup, 10))
+        pre = [next(it) for _ in range(nwarm + args.steps)]
+        loader.close()
+        # CSR pieces, labels and index arrays resident in HBM; the operand builder (the
+        # create_coo_tensor kernel) runs for every step, on the staging stream ahead of it
+        dbs = [lb.host.to_device(dev, build=False) for lb in pre]
+        torch.cuda.synchronize()
+        k_ = [0]
+
+        def nxt_pre():
+            j = k_[0]
+            k_[0] += 1
+            db = dbs[j]
+            return pre[j].plan, lambda: (db.build_operands(), db)[1]
+
+        pipeline(nxt_pre, nwarm)
+        cso.enable_timing(not args.no_roofline)
+        stager.timing = []
+        step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, args.steps))
+        cso.enable_timing(False)
+        recs = cso.take_timing_records()
+        h_bytes, h_sec = stager.take_timing()
+        gpu_step = {"value": round(world * args.steps / step_s, 3), "unit": "mini-batches/s",
+                    "ms_per_step": round(1e3 * step_s / args.steps, 3),
+                    "host_issue_ms_per_step": round(1e3 * step_issue / args.steps, 3),
+                    "what": f"{args.steps} distinct pre-sampled batches per rank (none cycled), CSR pieces resident "
+                            "in HBM; X0 staging, operand builds and the whole training step inside the timed region"}
+        staging_info = {"mode": args.staging, "host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
+                        "h2d_GBps": round(h_bytes / h_sec / 1e9, 1) if h_sec > 0 else None,
+                        "h2d_ms_per_batch": round(1e3 * h_sec / args.steps, 3),
+                        "note": ("GPU gather of the host rows from the pinned, device-mapped feature table over "
+                                 "PCIe" if args.staging == "zerocopy" else
+                                 "host rows gathered into pinned memory by the sampler threads, one hipMemcpyAsync")
+                                + " on the staging stream, overlapped with the previous step"}
+        step_batches = [lb.host for lb in pre[nwarm:]]
+        if recs:
+            roof, spmm_detail = roofline_from(recs, step_batches, args, traffic, args.steps)
+        if args.cprofile and rank == 0:
+            import cProfile
+            import pstats
+
+            k_[0] = 0
+            pr = cProfile.Profile()
+            pr.enable()
+            pipeline(nxt_pre, min(20, len(dbs)))
             torch.cuda.synchronize()
-        with open(args.torch_profile, "w") as fh:
-            fh.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60,
-                                                                        max_name_column_width=60,
-                                                                        max_shapes_column_width=90))
-            fh.write("\n\n")
-            fh.write(prof.key_averages().table(sort_by="count", row_limit=80, max_name_column_width=60))
-            fh.write("\n\n")
-            fh.write(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=50, max_name_column_width=60))
-            fh.write("\n\n")
-            for ev in prof.events():
-                if ev.device_type.name == "CUDA":
-                    continue
-                if ev.name in ("aten::mm", "aten::addmm", "aten::linear", "aten::matmul"):
-                    kern = [(k.name[:70], round(float(getattr(k, "duration", 0)), 1)) for k in ev.kernels]
-                    fh.write(f"{ev.name} {ev.input_shapes} {kern}\n")
+            pr.disable()
+            with open(args.cprofile, "w") as fh:
+                st = pstats.Stats(pr, stream=fh)
+                st.sort_stats("tottime").print_stats(45)
+                st.sort_stats("cumulative").print_stats(45)
+    else:
+        loader.close()
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
-    # ---------------------------------------------------------------- roofline
-    roof = None
-    spmm_detail = {}
-    if recs:
-        # per call site, in call order within a step: 3 forwards, then the backwards of
-        # layers 2 and 1 (layer 0's input needs no gradient)
-        names = ["fwd_L0", "fwd_L1", "fwd_L2", "bwd_L2", "bwd_L1"]
-        site, kname = {}, {}
-        for i, (tag, ms, nbytes, kn) in enumerate(recs):
-            key = names[i % len(names)]
-            assert key.startswith(tag), (key, tag)
-            e = site.setdefault(key, [0.0, 0, 0])
-            e[0] += ms
-            e[1] += nbytes
-            e[2] += 1
-            kname[key] = kn
-        for key, (ms, nbytes, n) in site.items():
-            spmm_detail[key] = {"avg_us": 1e3 * ms / n, "GB_per_launch": nbytes / n / 1e9,
-                                "GBps": nbytes / (ms * 1e-3) / 1e9, "kernel": kname[key]}
-        # the dominant kernel = the aggregation instantiation (as rocprofv3 names it) with the
-        # most time per step; several call sites may share it (rocprof averages over them too)
-        byk = {}
-        for key, (ms_, nb_, n_) in site.items():
-            e = byk.setdefault(kname[key], [0.0, 0, 0, []])
-            e[0] += ms_
-            e[1] += nb_
-            e[2] += n_
-            e[3].append(key)
-        dom = max(byk, key=lambda k_: byk[k_][0])
-        ms, nbytes, n, sites = byk[dom]
-        achieved = nbytes / (ms * 1e-3) / 1e9
-        tr = (traffic or {}).get("by_kernel", {}).get(dom)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                # GB per launch leaving L2 for the Infinity Cache / HBM (PMC, calibrated)
-                "traffic": round(tr["bytes_per_launch"] / 1e9, 4) if tr else None,
-                "kernel": f"{dom} (call sites {' + '.join(sorted(sites))}), avg {1e3 * ms / n:.1f} us/launch over "
-                          f"{n} launches, {nbytes / n / 1e9:.3f} GB algorithmic per launch"}
-        if tr:
-            roof["traffic_detail"] = dict(tr, read_correction=traffic["read_correction"],
-                                          write_correction=traffic["write_correction"],
-                                          all_kernels={k: round(v["bytes_per_launch"] / 1e9, 4)
-                                                       for k, v in traffic["by_kernel"].items()})
-        tot_ms = sum(v[0] for v in site.values())
-        tot_b = sum(v[1] for v in site.values())
-        roof["all_spmm_GBps"] = round(tot_b / (tot_ms * 1e-3) / 1e9, 1)
-        roof["spmm_ms_per_step"] = round(tot_ms / args.steps, 3)
-
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, host_batches[0], feats, num_classes)
+    sampler_cost = None
+    if rank == 0 and world == 1:
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, step_batches[0] if step_batches else probe_batch, feats, num_classes)
+        chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
+        t = time.perf_counter()
+        for i, c in enumerate(chunks[:3]):
+            fn(i, c, samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0])
+        nat = (time.perf_counter() - t) / 3
+        t = time.perf_counter()
+        fn(3, chunks[3], samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0], native=False)
+        sampler_cost = {"native_ms_per_batch_1thread": round(nat * 1e3, 1),
+                        "numpy_ms_per_batch_1thread": round((time.perf_counter() - t) * 1e3, 1)}
 
     if rank == 0:
-        value = world * args.steps / elapsed
         line = {
-            "metric": "mini-batches/sec + SpMM HBM GB/s, Reddit GraphSAGE/LADIES at 1/2/4/8 MI355X",
-            "value": round(value, 3),
+            "metric": METRIC,
+            "value": round(world * args.steps / e2e_s, 3),
             "unit": "mini-batches/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-            "host_issue_ms_per_step": round(1e3 * (t_issued - t_start) / args.steps, 3),
+            "ms_per_step": round(1e3 * e2e_s / args.steps, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic (Chung-Lu {spec.name}-shaped graph, N(0,1) features, random-init "
-                    f"{'GraphSAGE' if args.model == 'graphsage' else 'GCN'}); "
-                    f"{nb} pre-sampled {args.sampler} batches per rank cycled, operands resident in HBM",
-            "config": {"workload": (f"{GRAPH_NAMES[args.graph]} {'GraphSAGE' if args.model == 'graphsage' else 'GCN'} "
-                                    f"{args.sampler.upper() if args.sampler != 'fastgcn' else 'FastGCN'} "
-                                    f"samp_num={args.samp_num} batch_size={args.batch_size}"
-                                    + (" (BASELINE config 2)" if (args.model, args.sampler, args.samp_num,
-                                                                  args.batch_size) == ("graphsage", "ladies", 8192, 512)
-                                       and args.graph == "reddit" else "")),
-                       "sampler": args.sampler,
-                       "model": args.model, "global_batch": args.batch_size * world, "samp_num": args.samp_num,
-                       "nhid": args.nhid, "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
+                    f"{'GraphSAGE' if args.model == 'graphsage' else 'GCN'}); end to end: live {args.sampler} "
+                    f"sampling ({workers} sampler threads per rank) + host staging + H2D + the training step, "
+                    f"warm-up of {warm} steps drains the prefetch queue first",
+            "config": {"workload": workload_name(args, spec), "sampler": args.sampler, "model": args.model,
+                       "global_batch": args.batch_size * world, "samp_num": args.samp_num, "nhid": args.nhid,
+                       "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
-                       "nnz_per_batch": int(host_batches[0].nnz()),
-                       "fused_epilogue": not args.unfused},
+                       "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
+                       "sampler_workers_per_rank": workers},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "gpu_step": gpu_step,
+            "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "spmm_per_callsite": spmm_detail,
-            "end_to_end": e2e,
+            "sampler": sampler_cost,
             "feature_staging": staging_info,
             "final_loss": round(final_loss, 5),
         }

@@ -37,6 +37,7 @@ _SIGNATURES = {
     "gnn_spmm_config":(_INT, [_I64, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gnn_spmm_set_timing_events": (None, [_VP, _VP]),
     "gnn_segsort_workspace_bytes": (_SZ, [_I64]),
+    "gnn_build_operand_workspace_bytes": (_SZ, []),
     "gnn_build_operand_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
     "gnn_build_operand_t_f32": (_INT, [_VP, _VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP]),
     "gnn_build_operand_sorted_f32": (_INT, [_VP, _VP, _VP, _INT, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP]),

@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
       out_val[i] = (float)(inv * (double)normfact[c]);
     }
   }
-  if (__ballot(bad) != 0ull && lane == 0) atomicMax(flag, gen);
+  if (flag && __ballot(bad) != 0ull && lane == 0) atomicMax(flag, gen);
 }
 
 // Values of the transposed operand from its CSR structure (the CSC of A): entry i of
@@ -1220,32 +1220,6 @@ int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hi
   return 0;
 }
 
-// Per-device "unsorted row seen" word for the operand builder. Each build call takes a new
-// generation number; the flat pass raises the word to it (atomicMax) when it meets an
-// unsorted row and the fix pass runs only if the word is >= its generation. Concurrent
-// calls on other streams can only make a fix pass run needlessly, never skip a needed one.
-std::mutex g_flag_mu;
-unsigned long long* g_flag[64] = {};
-std::atomic<unsigned long long> g_gen{0};
-
-int operand_flag(unsigned long long** flag, unsigned long long* gen) {
-  int dev = 0;
-  GNN_HIP(hipGetDevice(&dev), "hipGetDevice");
-  GNN_REQUIRE(dev >= 0 && dev < 64, "operand builder: device id %d out of range", dev);
-  {
-    std::lock_guard<std::mutex> lk(g_flag_mu);
-    if (!g_flag[dev]) {
-      void* p = nullptr;
-      GNN_HIP(hipMalloc(&p, 256), "hipMalloc (operand flag)");
-      GNN_HIP(hipMemset(p, 0, 256), "hipMemset (operand flag)");
-      g_flag[dev] = (unsigned long long*)p;
-    }
-    *flag = g_flag[dev];
-  }
-  *gen = ++g_gen;
-  return 0;
-}
-
 }  // namespace
 
 // =================================================================================
@@ -1349,24 +1323,28 @@ size_t gnn_segsort_workspace_bytes(int64_t nseg) { return segsort_ws(nseg); }
 namespace {
 int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
                   const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col, float* csr_val,
-                  int64_t* coo_indices, bool sorted, void* stream);
+                  int64_t* coo_indices, unsigned long long* flag, void* stream);
 }  // namespace
+
+size_t gnn_build_operand_workspace_bytes(void) { return 256; }
 
 int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
                           const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col,
                           float* csr_val, int64_t* coo_indices, void* workspace, size_t workspace_bytes,
                           void* stream) {
-  (void)workspace;  // not needed (the unsorted-row flag lives in the library); ABI stability
-  (void)workspace_bytes;
+  // the "unsorted row seen" word lives in the caller's workspace, zeroed on the call's stream:
+  // no allocation inside the library, no state shared between concurrent calls
+  GNN_REQUIRE(nrows == 0 || nnz == 0 || (workspace != nullptr && workspace_bytes >= 8 && (uintptr_t)workspace % 8 == 0),
+              "gnn_build_operand_f32: needs an 8-byte aligned workspace of gnn_build_operand_workspace_bytes() bytes");
   return build_operand(fullrowptr, rowptr, colidx, colidx_bytes, normfact, nrows, ncols, nnz, csr_col, csr_val,
-                       coo_indices, false, stream);
+                       coo_indices, (unsigned long long*)workspace, stream);
 }
 
 int gnn_build_operand_sorted_f32(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx,
                                  int colidx_bytes, const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz,
                                  int32_t* csr_col, float* csr_val, int64_t* coo_indices, void* stream) {
   return build_operand(fullrowptr, rowptr, colidx, colidx_bytes, normfact, nrows, ncols, nnz, csr_col, csr_val,
-                       coo_indices, true, stream);
+                       coo_indices, nullptr, stream);
 }
 
 }  // extern "C"
@@ -1374,7 +1352,8 @@ int gnn_build_operand_sorted_f32(const int32_t* fullrowptr, const int32_t* rowpt
 namespace {
 int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* colidx, int colidx_bytes,
                   const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col, float* csr_val,
-                  int64_t* coo_indices, bool sorted, void* stream) {
+                  int64_t* coo_indices, unsigned long long* flag, void* stream) {
+  // flag == nullptr: rows guaranteed column-ascending (no check, no fix pass)
   GNN_REQUIRE(nrows >= 0 && ncols >= 0 && nnz >= 0, "gnn_build_operand_f32: negative size");
   GNN_REQUIRE(nrows < INT_MAX && ncols < INT_MAX && nnz < INT_MAX, "gnn_build_operand_f32: sizes must be < 2^31");
   GNN_REQUIRE(colidx_bytes == 2 || colidx_bytes == 4 || colidx_bytes == 8,
@@ -1383,9 +1362,9 @@ int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* 
   GNN_REQUIRE(fullrowptr && rowptr && colidx && normfact && csr_col && csr_val, "gnn_build_operand_f32: NULL input");
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)ceil_div(nrows, 4));
-  unsigned long long* flag = nullptr;
-  unsigned long long gen = 0;
-  if (int rc = operand_flag(&flag, &gen)) return rc;
+  const bool sorted = flag == nullptr;
+  const unsigned long long gen = 1;
+  if (!sorted) GNN_HIP(hipMemsetAsync(flag, 0, sizeof(*flag), st), "operand flag memset");
   const dim3 gflat((unsigned)ceil_div(nnz, 1024));  // 4 waves x 256 nonzeros
   const dim3 gfix(16);  // usually a no-op (gated): keep the launch small
   switch (colidx_bytes) {

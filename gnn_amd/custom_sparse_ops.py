@@ -16,12 +16,20 @@ tensor; the transpose needed by backward is built on the GPU once and cached too
 of the reference's per-backward ``A.transpose(0,1).coalesce()`` sort.
 
 Error behaviour mirrors the reference's TORCH_CHECKs (spmm.cpp:10-21): RuntimeError
-"<arg> must be a CUDA tensor" / "must be coalesced" / "must be contiguous". There is no CPU
-path: CPU tensors raise, as the reference's do.
+"<arg> must be a CUDA tensor" / "must be coalesced" / "must be contiguous".
+
+Device dispatch (BASELINE config 1, "single process on CPU via torch.sparse.mm"): when BOTH
+operands of ``spmm`` live on the CPU it runs the reference's own CPU expression
+(custom_sparse_ops.py:25,36: ``mat1.mm(mat2)`` forward, ``mat1.t().mm(grad)`` backward), and
+``create_coo_tensor`` with CPU inputs builds the COO with the same double-precision formula
+in torch. This is a device branch, not a fallback: a CUDA operand never leaves the HIP path
+(a missing libgnn_spmm.so raises), mixed devices raise, and the native entry points
+``spmm_load_balance`` / ``spmm_naive`` stay CUDA-only like spmm.cpp:10-21.
 """
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -44,17 +52,18 @@ def enable_timing(flag: bool = True) -> None:
 
 
 def take_timing_records(sync: bool = True):
-    """Return [(tag, ms, algorithmic_bytes, kernel_name)] for recorded calls and clear the list
-    (kernel_name as rocprofv3 lists the main kernel: spmm_unit_kernel<VW, G, NJ, U>).
+    """Return [(tag, ms, algorithmic_bytes, kernel_name, dims)] for recorded calls and clear
+    the list (kernel_name as rocprofv3 lists the main kernel: spmm_unit_kernel<VW, G, NJ, U>;
+    dims = {M, K, nnz, F, res_rows}: the call's shape, residual rows read if any).
 
     Also folds the times into spmm_forward_time / spmm_backward_time (seconds)."""
     global spmm_forward_time, spmm_backward_time
     if sync and _timing_records:
         _timing_records[-1][2].synchronize()
     out = []
-    for tag, e0, e1, nbytes, kname in _timing_records:
+    for tag, e0, e1, nbytes, kname, dims in _timing_records:
         ms = e0.elapsed_time(e1)
-        out.append((tag, ms, nbytes, kname))
+        out.append((tag, ms, nbytes, kname, dims))
         if tag.startswith("fwd"):
             spmm_forward_time += ms * 1e-3
         else:
@@ -87,7 +96,7 @@ class CsrOperand:
     rowptr int32[M+1], col int32[nnz], val fp32[nnz], columns ascending inside each row.
     ``transpose()`` returns (and caches) the canonical CSR of Aᵀ (K x M)."""
 
-    __slots__ = ("rowptr", "col", "val", "shape", "nnz", "_t", "__weakref__")
+    __slots__ = ("rowptr", "col", "val", "shape", "nnz", "_t", "_tw", "__weakref__")
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, shape: Tuple[int, int]):
         self.rowptr = rowptr
@@ -95,7 +104,9 @@ class CsrOperand:
         self.val = val
         self.shape = (int(shape[0]), int(shape[1]))
         self.nnz = int(col.numel())
-        self._t: Optional["CsrOperand"] = None
+        self._t: Optional["CsrOperand"] = None  # the cached transpose (strong)
+        self._tw = None  # on a transpose: weakref back to the operand it was made from (no cycle,
+        # so refcounting frees an operand pair as soon as the staged batch drops it)
 
     @property
     def device(self) -> torch.device:
@@ -109,7 +120,15 @@ class CsrOperand:
             ts += (self._t.rowptr, self._t.col, self._t.val)
         return ts
 
+    def _link(self, t: "CsrOperand") -> None:
+        self._t = t
+        t._tw = weakref.ref(self)
+
     def transpose(self) -> "CsrOperand":
+        if self._t is None and self._tw is not None:
+            back = self._tw()
+            if back is not None:
+                return back
         if self._t is None:
             M, K = self.shape
             dev = self.device
@@ -123,9 +142,7 @@ class CsrOperand:
                 _lib.check(L.gnn_csr_transpose(_ptr(self.rowptr), _ptr(self.col), _ptr(self.val), M, K, self.nnz,
                                                _ptr(tr_rowptr), _ptr(tr_col), _ptr(tr_val), _ptr(ws), wsb,
                                                _stream(dev)), "gnn_csr_transpose")
-            t = CsrOperand(tr_rowptr, tr_col, tr_val, (K, M))
-            t._t = self
-            self._t = t
+            self._link(CsrOperand(tr_rowptr, tr_col, tr_val, (K, M)))
         return self._t
 
     def to_torch_coo(self) -> torch.Tensor:
@@ -230,7 +247,9 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
                 nbytes += residual.shape[0] * F * 4 + M * 4
             res = "true" if rmap is not None else "false"
             _timing_records.append((tag, e0, e1, nbytes,
-                                    f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>"))
+                                    f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>",
+                                    dict(M=M, K=K, nnz=op.nnz, F=F,
+                                         res_rows=residual.shape[0] if rmap is not None else 0)))
         if rmap is None:
             _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
                                           dense.data_ptr(), ldx, out.data_ptr(), ldo, Fk,
@@ -244,11 +263,22 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
     return out if Fk == F else out[:, :F]
 
 
+def _on_cpu(mat1, mat2) -> bool:
+    """Both operands on the CPU: the config-1 torch.sparse.mm branch."""
+    return (isinstance(mat1, torch.Tensor) and isinstance(mat2, torch.Tensor) and mat1.device.type == "cpu"
+            and mat2.device.type == "cpu")
+
+
 class SparseDenseMM(torch.autograd.Function):
     """custom_sparse_ops.py:16-37: forward A·X, backward (None, Aᵀ·G)."""
 
     @staticmethod
     def forward(ctx, mat1, mat2):
+        if _on_cpu(mat1, mat2):
+            # custom_sparse_ops.py:25 (the reference's CPU expression)
+            _require(mat1.is_sparse, "sparseMat must be a sparse COO tensor")
+            ctx.cpu_mat1 = mat1
+            return torch.sparse.mm(mat1, mat2)
         op = csr_of(mat1)
         _require(mat2.is_cuda, "denseMat must be a CUDA tensor")
         ctx.op = op
@@ -258,6 +288,9 @@ class SparseDenseMM(torch.autograd.Function):
     def backward(ctx, grad_output):
         if not ctx.needs_input_grad[1]:
             return None, None
+        if getattr(ctx, "cpu_mat1", None) is not None:
+            # custom_sparse_ops.py:36, with the coalesce() torch needs for a transposed COO
+            return None, torch.sparse.mm(ctx.cpu_mat1.t().coalesce(), grad_output.contiguous())
         op_t = ctx.op.transpose()
         return None, spmm_csr(op_t, grad_output.contiguous(), tag="bwd")
 
@@ -305,9 +338,11 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
                 _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
                 nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _stream(dev)), "gnn_build_operand_sorted_f32")
         else:
+            wsb = _lib.lib().gnn_build_operand_workspace_bytes()
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)  # the unsorted-row flag
             _lib.check(_lib.lib().gnn_build_operand_f32(
                 _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
-                nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), None, 0, _stream(dev)),
+                nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _ptr(ws), wsb, _stream(dev)),
                 "gnn_build_operand_f32")
     return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
 
@@ -328,15 +363,31 @@ def attach_transpose(op: CsrOperand, fullrowptr: torch.Tensor, colptr: torch.Ten
                                                       M, K, op.nnz, _ptr(val), _stream(dev)),
                    "gnn_build_operand_t_f32")
     t = CsrOperand(colptr, rows, val, (K, M))
-    t._t = op
-    op._t = t
+    op._link(t)
     return t
+
+
+def _create_coo_tensor_cpu(fullrowptr, rowptr, colidx, normfact, nrows: int, ncols: int) -> torch.Tensor:
+    """The config-1 CPU branch of create_coo_tensor: cuda_spmm.cu:795-802's formula in torch,
+    value = (float)((1.0 / full_degree(row)) * (double)normfact[col]) (two double roundings
+    then one to fp32, the same operations as the HIP builder), then .coalesce()
+    (cuda_spmm.cu:825)."""
+    rp = rowptr.to(torch.int64)
+    rows = torch.repeat_interleave(torch.arange(nrows, dtype=torch.int64), rp[1:] - rp[:-1])
+    col = colidx.to(torch.int64)  # int16 sign-extends like the reference's accessor
+    deg = (fullrowptr[1:] - fullrowptr[:-1]).to(torch.float64)
+    val = ((1.0 / deg)[rows] * normfact.to(torch.float64)[col]).to(torch.float32)
+    return torch.sparse_coo_tensor(torch.stack([rows, col]), val, (nrows, ncols)).coalesce()
 
 
 def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> torch.Tensor:
     """spmm.cpp:44-50 / cuda_spmm.cu:806-827: coalesced sparse COO of the sampled layer with
     value = (1/full_degree(row)) * normfact[col] (double math, fp32 store). The CSR image
-    is cached on the returned tensor for the aggregation kernels."""
+    is cached on the returned tensor for the aggregation kernels. CPU inputs (all four)
+    take the config-1 CPU branch."""
+    ins = (fullrowptr, rowptr, colidx, normfact)
+    if all(isinstance(t, torch.Tensor) and t.device.type == "cpu" for t in ins):
+        return _create_coo_tensor_cpu(*ins, int(nrows), int(ncols))
     op, coo = build_operand(fullrowptr, rowptr, colidx, normfact, int(nrows), int(ncols), with_coo=True)
     t = torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols)), is_coalesced=True)
     t._gnn_csr = op

@@ -37,6 +37,11 @@ PRODUCTS = GraphSpec("ogbn-products", 2_449_029, 61_859_140, 100, 47, 0.08, 0.01
 # ogbn-papers100M per-batch geometry on a graph scaled to fit the box (128 feats, 172 classes).
 PAPERS_SCALED = GraphSpec("ogbn-papers100M-scaled", 4_000_000, 60_000_000, 128, 172, 0.011, 0.001)
 TINY = GraphSpec("tiny", 3_000, 15_000, 602, 41, 0.66, 0.1)
+# Per-batch geometry of configs 3-5 at a size the GPU parity tests build in seconds: the same
+# expected degree (edge samples per node) and feature / class widths on 500 k nodes, so a
+# LADIES / FastGCN batch (samp 8192, batch 512) has the full-size layer shapes.
+PRODUCTS_TEST = GraphSpec("ogbn-products-test", 500_000, 500_000 * 61_859_140 // 2_449_029, 100, 47, 0.08, 0.016)
+PAPERS_TEST = GraphSpec("ogbn-papers100M-test", 500_000, 500_000 * 60_000_000 // 4_000_000, 128, 172, 0.011, 0.001)
 
 
 def chung_lu(num_nodes: int, num_edge_samples: int, sigma: float, rng: np.random.Generator) -> sp.csr_matrix:
@@ -80,3 +85,13 @@ def row_normalize(mx: sp.spmatrix) -> sp.csr_matrix:
         r_inv = np.power(rowsum, -1).flatten()
     r_inv[np.isinf(r_inv)] = 0.0
     return sp.diags(r_inv).dot(mx).tocsr()
+
+
+def lap_matrix(A: sp.spmatrix, model: str) -> sp.csr_matrix:
+    """main.py:267-270: row_normalize(A) for GraphSAGE, row_normalize(A + I) for GCN
+    (canonical CSR: duplicates summed, indices sorted)."""
+    if model == "gcn":
+        A = A + sp.eye(A.shape[0], dtype=A.dtype, format="csr")
+    lap = row_normalize(A)
+    lap.sum_duplicates()
+    return lap

@@ -87,6 +87,23 @@ class HostBatch:
             self.extra["rmaps"] = rm
         return self
 
+    def cpu_inputs(self, feat_data: torch.Tensor):
+        """BASELINE config 1 (single process on the CPU): (adjs, x0, sampled_nodes, labels)
+        with the operands built by create_coo_tensor's CPU branch and X0 = the layer-0 input
+        rows of the host feature table (main.py:129-134 with every row on the host)."""
+        from . import custom_sparse_ops as cso
+
+        adjs = []
+        for L in self.layers:
+            if L is None:
+                adjs.append(None)
+                continue
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+            adjs.append(cso.create_coo_tensor(t(L.fullrowptr), t(L.rowptr), t(L.colidx), t(L.normfact), *L.shape))
+        x0 = feat_data[torch.from_numpy(np.asarray(self.input_nodes, dtype=np.int64))]
+        sampled = [torch.from_numpy(np.asarray(s, dtype=np.int64)) for s in self.sampled_nodes]
+        return adjs, x0, sampled, torch.from_numpy(self.labels)
+
     def to_device(self, device, with_coo: bool = True, build: bool = True):
         """Materialise on the GPU (H2D of the CSR pieces, labels, sampled_nodes) and, unless
         build=False, run the operand builder. Returns a DeviceBatch."""

@@ -114,7 +114,6 @@ class StagePlan:
     peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
     pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos[, host_src])
-    peer_meta: Optional[tuple] = None  # PeerExchange.prepare: (send counts, recv counts, want, pos)
 
 
 def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devices=None) -> StagePlan:
@@ -166,8 +165,11 @@ class Stager:
         compute stream after all of it."""
         dev = self.device
         st = self.stream
+        meta = None
         if self.exchange is not None:
-            self.exchange.prepare(plan)  # host-side metadata all-to-all (gloo), in batch order
+            # host-side metadata all-to-all (gloo), in batch order, paid for every issue: the
+            # negotiation is part of each step (never cached on a plan that is issued again)
+            meta = self.exchange.prepare(plan)
         # No wait on the compute stream: staging only reads static buffers and its own
         # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
@@ -191,7 +193,7 @@ class Stager:
                 cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
             extra = ()
             if self.exchange is not None:
-                extra = self.exchange.exchange(plan, x0, self.store)
+                extra = self.exchange.exchange(plan, x0, self.store, meta)
             batch = batch_fn() if batch_fn is not None else None
             ev = torch.cuda.Event()
             ev.record(st)
@@ -282,11 +284,10 @@ class PeerExchange:
             meta_group = group if dist.get_backend(group) == "gloo" else dist.new_group(backend="gloo")
         self.meta_group = meta_group
 
-    def prepare(self, plan: StagePlan) -> None:
-        """Host-side negotiation for one batch (idempotent). Collective: call on every rank,
-        for the same batch sequence."""
-        if getattr(plan, "peer_meta", None) is not None:
-            return
+    def prepare(self, plan: StagePlan) -> tuple:
+        """Host-side negotiation for one batch: (send counts, recv counts, wanted slots, X0
+        positions). Collective: call on every rank, for the same batch sequence, once per
+        exchange (the result is not cached: every step pays its own negotiation)."""
         dist, W = self.dist, self.world
         sc = [len(plan.peer_src[j]) for j in range(W)]
         rc_t = torch.empty(W, dtype=torch.int64)
@@ -297,11 +298,10 @@ class PeerExchange:
         dist.all_to_all_single(want, req, output_split_sizes=rc, input_split_sizes=sc, group=self.meta_group)
         pos = torch.from_numpy(np.concatenate(plan.peer_pos).astype(np.int64) if W else np.zeros(0, np.int64))
         pin = torch.cuda.is_available()
-        plan.peer_meta = (sc, rc, want.pin_memory() if pin else want, pos.pin_memory() if pin else pos)
+        return (sc, rc, want.pin_memory() if pin else want, pos.pin_memory() if pin else pos)
 
-    def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore):
-        self.prepare(plan)
-        sc, rc, want_h, pos_h = plan.peer_meta
+    def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore, meta: Optional[tuple] = None):
+        sc, rc, want_h, pos_h = self.prepare(plan) if meta is None else meta
         dev = x0.device
         want = want_h.to(dev, non_blocking=True)
         pos = pos_h.to(dev, non_blocking=True)

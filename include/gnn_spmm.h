@@ -98,10 +98,13 @@ void gnn_spmm_set_timing_events(void* start, void* stop);
  * (cuda_spmm.cu:825); rows are assumed free of duplicate columns (scipy slicing output).
  * Outputs: csr_col (int32, nnz), csr_val (fp32, nnz) and, if coo_indices != NULL, the
  * coalesced COO indices int64[2][nnz] (row-major: all rows then all columns).
- * `workspace` is not used any more (rows are sorted inside the build kernel) and may be
- * NULL; the parameter is kept for ABI stability.
+ * `workspace` (device, 8-byte aligned, >= gnn_build_operand_workspace_bytes()) holds the
+ * call's "unsorted row seen" word, zeroed on `stream` by the call itself: the library keeps
+ * no device state and allocates nothing, so the call is graph-capturable and concurrent
+ * calls on different streams need different workspaces.
  * ------------------------------------------------------------------------------- */
 size_t gnn_segsort_workspace_bytes(int64_t nseg);
+size_t gnn_build_operand_workspace_bytes(void);
 int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr,
                           const void* colidx, int colidx_bytes,
                           const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz,

@@ -99,9 +99,9 @@ def _exchange_worker(rank, world, port, q):
                              torch.zeros(0, F), peer_pos, peer_src)
     x0 = torch.full((n_in, 8), -1.0)
     ex = staging.PeerExchange()
-    ex.prepare(plan)
-    ex.prepare(plan)  # idempotent
-    ex.exchange(plan, x0, store)
+    meta = ex.prepare(plan)
+    assert ex.prepare(plan)[:2] == meta[:2]  # same negotiation when repeated
+    ex.exchange(plan, x0, store, meta)
     expect = torch.arange(k * F, dtype=torch.float32).view(k, F)[torch.from_numpy(src)] + 1000 * peer
     ok = torch.equal(x0[torch.from_numpy(pos), :F], expect)
     q.put((rank, ok))

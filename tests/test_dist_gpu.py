@@ -1,0 +1,204 @@
+"""GPU, world_size 2: the data-parallel step the benchmark runs at N > 1, on the one GPU.
+
+Both ranks run on cuda:0 with GNN_DIST_BACKEND=gloo (RCCL refuses two ranks on one GPU;
+gloo moves the same CUDA tensors through the host), spawned as fresh processes.
+
+* Trainer on CUDA: the native branch — ClipAdam.clip_to_flat (this rank's clip_grad_norm_(5)
+  written into the flat all-reduce buffer), all_reduce(SUM), ClipAdam.step(clipped=True) —
+  for 2 steps on rank-specific batches (the reference's LADIES goldens c2 / c3) must equal the
+  reference's semantics computed independently in this process on the CPU (main.py:146-170:
+  per-rank clip, SUM over ranks, no averaging, then Adam; initial weights broadcast from rank 0),
+  through the product's CPU branch (torch.sparse.mm) and torch.optim.Adam.
+  Tolerance: parameters within rtol 1e-4 / atol 1e-6 where the summed gradient is clearly
+  non-zero (Adam's first steps move a weight by ~lr·sign(g), so weights whose gradient sits at
+  the fp32 noise level are excluded, as in tests/test_fused_gpu.py).
+* PeerExchange with the HIP gathers: every rank receives exactly the rows it requested from
+  the peer's GPU buffer (bit-exact), through the per-step host negotiation + all_to_all.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = (2, 3)  # ladies_tiny cases per rank
+LR = 0.01
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(rank, device):
+    z = np.load(os.path.join(GOLDEN, "ladies_tiny.npz"))
+    c = CASES[rank]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    adjs = [torch.sparse_coo_tensor(t(z[f"c{c}_adj{li}_indices"]), t(z[f"c{c}_adj{li}_values"]),
+                                    tuple(int(v) for v in z[f"c{c}_adj{li}_shape"])).coalesce() for li in range(3)]
+    sampled = [t(z[f"c{c}_sampled{li}"]) for li in range(3)]
+    g = torch.Generator().manual_seed(77 + rank)
+    x0 = torch.randn(int(z[f"c{c}_nin"]), 602, generator=g)
+    y = t(z[f"c{c}_labels"])
+    if device != "cpu":
+        adjs = [a.to(device) for a in adjs]
+        sampled = [s.to(device) for s in sampled]
+        x0, y = x0.to(device), y.to(device)
+    return adjs, x0, sampled, y
+
+
+def _model(seed):
+    from gnn_amd.models import build_model
+
+    torch.manual_seed(seed)
+    # dropout 0: the CPU reference and the GPU run draw no masks (their RNGs differ)
+    return build_model("graphsage", 602, 32, [1, 1, 1], 41, dropout=0.0)
+
+
+def _env(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), GNN_DIST_BACKEND="gloo")
+
+
+def _trainer_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+
+    try:
+        from gnn_amd.models import build_model
+        from gnn_amd.train import Trainer, init_distributed
+
+        init_distributed()
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(100 + rank)  # a different init per rank: the broadcast must fix it
+        net = build_model("graphsage", 602, 32, [1, 1, 1], 41, dropout=0.0, fused=True).to(dev)
+        tr = Trainer(net, LR, dev)
+        assert tr.native and tr.world == world
+        adjs, x0, sampled, y = _inputs(rank, dev)
+        losses = [float(tr.step(x0, adjs, sampled, y)) for _ in range(2)]
+        torch.cuda.synchronize()
+        q.put((rank, "ok", losses, [p.detach().cpu().numpy().copy() for p in net.parameters()]))
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, f"error: {e!r}", None, None))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _exchange_worker(rank, world, port, q):
+    _env(rank, world, port)
+    import torch.distributed as dist
+
+    try:
+        from gnn_amd import staging
+        from gnn_amd.train import init_distributed
+
+        init_distributed()
+        dev = torch.device("cuda", 0)
+        F, k, n_in = 602, 300, 500
+        feats = torch.arange(2 * k * F, dtype=torch.float32).view(2 * k, F) * 1e-3
+        # rank r buffers nodes [r*k, (r+1)*k) of the feature table, slot i = node r*k + i
+        store = staging.FeatureStore(feats, np.arange(rank * k, (rank + 1) * k), dev, rank)
+        rng = np.random.default_rng(rank)
+        peer = 1 - rank
+        pos = np.sort(rng.choice(n_in, 200, replace=False)).astype(np.int64)
+        src = rng.integers(0, k, 200).astype(np.int64)
+        empty = np.zeros(0, np.int64)
+        peer_pos, peer_src = [empty, empty], [empty, empty]
+        peer_pos[peer], peer_src[peer] = pos, src
+        plan = staging.StagePlan(n_in, empty, empty, empty, None, peer_pos, peer_src)
+        x0 = torch.full((n_in, store.ld), -1.0, device=dev)
+        ex = staging.PeerExchange()
+        for _ in range(2):  # negotiated afresh each time
+            ex.exchange(plan, x0, store)
+        torch.cuda.synchronize()
+        expect = feats[torch.from_numpy(peer * k + src)]
+        ok = torch.equal(x0[torch.from_numpy(pos).to(dev), :F].cpu(), expect)
+        untouched = np.setdiff1d(np.arange(n_in), pos)
+        ok = ok and bool((x0[torch.from_numpy(untouched).to(dev)] == -1.0).all())
+        q.put((rank, "ok" if ok else "rows differ", None, None))
+    except Exception as e:
+        q.put((rank, f"error: {e!r}", None, None))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(fn, world=2):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = [q.get(timeout=100) for _ in range(world)]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    return sorted(out, key=lambda t: t[0])
+
+
+def _reference_two_steps():
+    """main.py:146-170 on the CPU: per-rank grads, per-rank clip_grad_norm_(5), SUM, Adam."""
+    from gnn_amd.models import loss as loss_fn
+
+    nets = [_model(100) for _ in range(2)]  # rank 0's init on both (the broadcast)
+    params = list(nets[0].parameters())
+    opt = torch.optim.Adam(params, lr=LR)
+    inputs = [_inputs(r, "cpu") for r in range(2)]
+    sums = []
+    for _ in range(2):
+        with torch.no_grad():
+            for p0, p1 in zip(nets[0].parameters(), nets[1].parameters()):
+                p1.copy_(p0)
+        grads = []
+        for r in range(2):
+            net = nets[r]
+            net.zero_grad()
+            adjs, x0, sampled, y = inputs[r]
+            lo = loss_fn(net(x0, adjs, sampled), y, True, "cpu")
+            lo.backward()
+            torch.nn.utils.clip_grad_norm_(net.parameters(), 5)
+            grads.append([p.grad.detach().clone() for p in net.parameters()])
+        total = [a + b for a, b in zip(*grads)]
+        for p, g in zip(params, total):
+            p.grad = g
+        sums.append(total)
+        opt.step()
+    return [p.detach().numpy() for p in params], sums
+
+
+def test_trainer_native_dp_step_matches_reference():
+    out = _spawn(_trainer_worker)
+    for rank, status, _, _ in out:
+        assert status == "ok", f"rank {rank}: {status}"
+    ref, sums = _reference_two_steps()
+    p0, p1 = out[0][3], out[1][3]
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b), "ranks disagree after the summed update"
+    for i, (got, want) in enumerate(zip(p0, ref)):
+        sure = np.ones(got.shape, bool)
+        for s in sums:
+            gg = s[i].numpy()
+            sure &= np.abs(gg) > 1e-4 * max(np.abs(gg).max(), 1e-12)
+        assert sure.mean() > 0.5
+        np.testing.assert_allclose(got[sure], want[sure], rtol=1e-4, atol=1e-6, err_msg=f"param {i}")
+
+
+def test_peer_exchange_hip_gathers_bit_exact():
+    out = _spawn(_exchange_worker)
+    for rank, status, _, _ in out:
+        assert status == "ok", f"rank {rank}: {status}"
