@@ -434,8 +434,13 @@ def test_errors(dev):
     A = torch.sparse_coo_tensor(torch.tensor([[1, 0], [0, 1]]), torch.tensor([1.0, 2.0]), (2, 2))
     with pytest.raises(RuntimeError, match="coalesced"):
         cso.spmm(A.to(dev), torch.randn(2, 3, device=dev))
+    # both operands on the CPU is the config-1 torch.sparse.mm branch; a mixed pair raises
     with pytest.raises(RuntimeError, match="CUDA"):
-        cso.spmm(A.coalesce(), torch.randn(2, 3))
+        cso.spmm(A.coalesce(), torch.randn(2, 3, device=dev))
+    with pytest.raises(RuntimeError, match="CUDA"):
+        cso.spmm(A.coalesce().to(dev), torch.randn(2, 3))
+    with pytest.raises(RuntimeError, match="CUDA"):
+        cso.spmm_load_balance(A.coalesce(), torch.randn(2, 3))
     with pytest.raises(RuntimeError, match="contiguous"):
         cso.spmm_load_balance(A.coalesce().to(dev), torch.randn(3, 2, device=dev).t())
     with pytest.raises(RuntimeError, match="size mismatch"):
