@@ -133,6 +133,29 @@ __device__ __forceinline__ int wave_first_true(int lo, int hi, int lane, Pred pr
 // ---------------------------------------------------------------------------------
 constexpr int ROW_UNIT = 64;
 
+// Workgroup -> (unit block, column tile). The launch is 1-D; workgroups are dealt to the 8
+// XCDs round-robin (b and b + 8 share one, MI355X_MICROARCH.md §Workgroup dispatch), and
+// each XCD has its own 4 MiB L2. In tile-major order (xcd_chunk == 0) all 8 XCDs sweep the
+// same column tile at once, so every L2 must hold that tile's whole slice of X. With the
+// XCD map the tile-major list of W = gx * tiles items is cut into 8 contiguous chunks of
+// xcd_chunk items and workgroup b works on item (b % 8) * xcd_chunk + b / 8: each XCD walks
+// its own chunk in order, i.e. its own tile at a time, and holds only that tile's slice.
+struct WorkMap {
+  int gx;         // unit blocks per column tile (incl. the row-unit blocks)
+  int items;      // gx * tiles
+  int xcd_chunk;  // 0: tile-major order; else ceil(items / 8)
+  __device__ __forceinline__ bool locate(unsigned b, int& ub, int& tile) const {
+    int w = (int)b;
+    if (xcd_chunk) {
+      w = (int)(b & 7u) * xcd_chunk + (int)(b >> 3);
+      if (w >= items) return false;
+    }
+    tile = w / gx;
+    ub = w - tile * gx;
+    return true;
+  }
+};
+
 template <int VW, int G, int NJ, int U, bool RES>
 __global__ __launch_bounds__(256) void spmm_unit_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
@@ -140,14 +163,16 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
     const float* __restrict__ X, int64_t ldx,
     float* __restrict__ Y, int64_t ldy,
     float* __restrict__ slab, int64_t ldslab, int F,
-    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
+    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap, WorkMap wm) {
   using V = typename Vec<VW>::T;
   constexpr int P = 64 / G;            // nonzeros taken side by side per step
   constexpr int COVER = VW * G * NJ;   // columns covered by one column tile
   const int lane = threadIdx.x & 63;
-  const int u = blockIdx.x * 4 + (threadIdx.x >> 6);  // wave-uniform; no block barriers below
+  int ub, tile;
+  if (!wm.locate(blockIdx.x, ub, tile)) return;
+  const int u = ub * 4 + (threadIdx.x >> 6);  // wave-uniform; no block barriers below
   const int sub = lane / G;
-  const int c0 = blockIdx.y * COVER + (lane % G) * VW;
+  const int c0 = tile * COVER + (lane % G) * VW;
   if (u >= nunits) {  // row unit: the empty rows among ROW_UNIT consecutive rows
     const int r0 = (u - nunits) * ROW_UNIT;
     if (r0 >= M) return;
@@ -1130,8 +1155,20 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
   return c;
 }
 
+// The XCD map pays when a column tile's slice of X is re-read (several tiles, many units);
+// GNN_SPMM_XCD=0/1 forces it off/on (measurements).
+WorkMap work_map(const SpmmCfg& c, int64_t M) {
+  WorkMap wm{};
+  wm.gx = (int)ceil_div(c.nunits + ceil_div(M, (int64_t)ROW_UNIT), 4);
+  wm.items = wm.gx * c.tiles;
+  bool on = c.tiles > 1;
+  if (const char* e = getenv("GNN_SPMM_XCD")) on = atoi(e) != 0;
+  wm.xcd_chunk = on ? (int)ceil_div(wm.items, 8) : 0;
+  return wm;
+}
+
 using MainFn = void (*)(const int*, const int*, const float*, int, int, int, int, const float*, int64_t,
-                        float*, int64_t, float*, int64_t, int, const float*, int64_t, const int*);
+                        float*, int64_t, float*, int64_t, int, const float*, int64_t, const int*, WorkMap);
 
 constexpr int pick_u(int nj) { return nj <= 4 ? 4 : (nj == 5 ? 3 : 2); }
 
@@ -1291,10 +1328,13 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
   GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no kernel for vw=%d g=%d nj=%d", c.vw, c.g, c.nj);
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
-  const dim3 grid((unsigned)ceil_div(c.nunits + ceil_div(M, (int64_t)ROW_UNIT), 4), (unsigned)c.tiles);
+  GNN_REQUIRE(ceil_div(c.nunits + ceil_div(M, (int64_t)ROW_UNIT), 4) * c.tiles < (int64_t)INT_MAX - 8,
+              "gnn_spmm_csr_f32: grid too large");
+  const WorkMap wm = work_map(c, M);
+  const dim3 grid((unsigned)(wm.xcd_chunk ? 8 * (int64_t)wm.xcd_chunk : wm.items));
   if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
   hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
-                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap);
+                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap, wm);
   GNN_LAUNCHED("spmm_unit_kernel");
   if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
