@@ -88,6 +88,9 @@ def parse():
                     help="non-buffered feature rows: host gather into pinned memory + one hipMemcpyAsync "
                          "(copy), or the GPU reads the mapped host table over PCIe (zerocopy: measured "
                          "slower, it slows the concurrent compute kernels)")
+    ap.add_argument("--host-extract", action="store_true",
+                    help="LADIES: extract every layer's sub-graph on the host (sampler threads) instead of "
+                         "leaving the layers below the top one to the GPU extraction (gnn_ladies_extract_f32)")
     ap.add_argument("--cprofile", default="", help="after the timed runs, cProfile 20 GPU steps into this file")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     a = ap.parse_args()
@@ -113,7 +116,10 @@ def _counter_rows(d):
 def _kernel_symbol(name: str) -> str:
     """'void (anonymous namespace)::spmm_unit_kernel<4, 16, 1, 4, false>(int const*, ...)' ->
     'spmm_unit_kernel<4, 16, 1, 4, false>' (the form the bench's timing records use)."""
-    name = name.split("(anonymous namespace)::")[-1]
+    if name.startswith("void "):
+        name = name[5:]
+    if name.startswith("(anonymous namespace)::"):
+        name = name[len("(anonymous namespace)::"):]
     depth = 0
     for i, ch in enumerate(name):
         if ch == "<":
@@ -321,13 +327,17 @@ def roofline_from(recs, step_batches, args, traffic, steps):
     for i, (tag, ms, nbytes, kn, dims) in enumerate(recs):
         key = names[i % len(names)]
         assert key.startswith(tag), (key, tag)
-        hb = step_batches[(i // len(names)) % len(step_batches)]
+        hb, db = step_batches[(i // len(names)) % len(step_batches)]
         li = int(key[-1])
         L = hb.layers[li]
         ck = (id(hb), key)
         if ck not in uniq_cache:  # distinct X rows the call gathers (cols of A, or non-empty rows for Aᵀ)
-            uniq_cache[ck] = (np.unique(L.colidx).size if key.startswith("fwd")
-                              else int(np.count_nonzero(np.diff(L.rowptr))))
+            if L.on_device:  # GPU-extracted: the column counts (host) / the device row pointer
+                uniq_cache[ck] = (int(np.count_nonzero(np.diff(L.csc_colptr))) if key.startswith("fwd")
+                                  else int(torch.count_nonzero(torch.diff(db.adjs[li].rowptr)).item()))
+            else:
+                uniq_cache[ck] = (np.unique(L.colidx).size if key.startswith("fwd")
+                                  else int(np.count_nonzero(np.diff(L.rowptr))))
         F, M, nnz = dims["F"], dims["M"], dims["nnz"]
         comp = uniq_cache[ck] * F * 4 + nnz * 8 + (M + 1) * 4 + M * F * 4 + dims["res_rows"] * F * 4
         if dims["res_rows"]:
@@ -496,8 +506,13 @@ def main():
     from gnn_amd.loader import BatchLoader
 
     workers = args.workers or default_workers(world)
+    dx = args.sampler == "ladies" and not args.host_extract
     loader = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank,
-                         world_size=world, store=store, workers=workers, seed=4242, kind=args.sampler)
+                         world_size=world, store=store, workers=workers, seed=4242, kind=args.sampler,
+                         device_extract=dx)
+    if dx:  # the graph resident in HBM for the extraction (made once, outside every timed region)
+        sampler.device_graph(loader.graph, dev)
+        torch.cuda.synchronize()
     it = loader.forever()
 
     def nxt_live():
@@ -549,7 +564,7 @@ def main():
                                  "PCIe" if args.staging == "zerocopy" else
                                  "host rows gathered into pinned memory by the sampler threads, one hipMemcpyAsync")
                                 + " on the staging stream, overlapped with the previous step"}
-        step_batches = [lb.host for lb in pre[nwarm:]]
+        step_batches = [(lb.host, db) for lb, db in zip(pre[nwarm:], dbs[nwarm:])]
         if recs:
             roof, spmm_detail = roofline_from(recs, step_batches, args, traffic, args.steps)
         if args.cprofile and rank == 0:
@@ -574,7 +589,7 @@ def main():
     sampler_cost = None
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, step_batches[0] if step_batches else probe_batch, feats, num_classes)
+            cpu = cpu_baseline(args, probe_batch, feats, num_classes)
         chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
         t = time.perf_counter()
         for i, c in enumerate(chunks[:3]):
@@ -584,6 +599,13 @@ def main():
         fn(3, chunks[3], samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0], native=False)
         sampler_cost = {"native_ms_per_batch_1thread": round(nat * 1e3, 1),
                         "numpy_ms_per_batch_1thread": round((time.perf_counter() - t) * 1e3, 1)}
+        if dx:
+            t = time.perf_counter()
+            for i, c in enumerate(chunks[:3]):
+                fn(i, c, samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0], device_extract=True)
+            sampler_cost["native_draw_only_ms_per_batch_1thread"] = round((time.perf_counter() - t) / 3 * 1e3, 1)
+            sampler_cost["note"] = ("native: host extraction of every layer; draw_only: the layers below the top "
+                                    "one left to the GPU extraction (what the end-to-end run uses)")
 
     if rank == 0:
         line = {
@@ -607,7 +629,8 @@ def main():
                        "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
-                       "sampler_workers_per_rank": workers},
+                       "sampler_workers_per_rank": workers,
+                       "layer_extraction": "gpu (layers below the top one)" if dx else "host"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,

@@ -66,6 +66,9 @@ _SIGNATURES = {
                                     ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _VP, _VP]),
     "gnn_head_bce_bwd_f32": (_INT, [_VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _VP, ctypes.c_float,
                                     ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _I64, _VP]),
+    # include/gnn_extract.h
+    "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP,
+                                      _VP, _VP, _VP, _VP, _VP, _VP]),
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
     "gnn_gemm_f32_split3_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
@@ -81,6 +84,9 @@ _SAMPLER_SIGNATURES = {
     "gnn_sampler_last_error": (ctypes.c_char_p, []),
     "gnn_ladies_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                  ctypes.POINTER(_VP)]),
+    "gnn_ladies_sample_dev": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
+                                     ctypes.c_int32, ctypes.POINTER(_VP)]),
+    "gnn_ladies_layer_device": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP]),
     "gnn_subgraph_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                    ctypes.POINTER(_VP)]),
     "gnn_fastgcn_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,

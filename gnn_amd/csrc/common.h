@@ -16,6 +16,9 @@ int fail(int code, const char* fmt, ...);
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// out[0..n] = exclusive prefix of in[0..n) (out[n] = total), one workgroup (spmm.hip).
+int launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st);
+
 }  // namespace gnn
 
 #define GNN_REQUIRE(cond, ...)                              \

@@ -80,10 +80,12 @@ class MT19937 {
 
 struct Layer {
   bool present = false;
-  int64_t M = 0, K = 0, s_num = 0;
+  bool on_device = false;  // entries left to the GPU extraction (gnn_ladies_extract_f32)
+  int64_t M = 0, K = 0, s_num = 0, nnz = 0;
   std::vector<int32_t> fullrowptr, rowptr, colidx;
   std::vector<float> normfact;
   std::vector<int64_t> sampled;
+  std::vector<int32_t> rows, cols, colptr;  // on_device: U's rows, after_nodes, CSC column pointer
 };
 
 // RandomState.choice(N, size, p=p, replace=False) (numpy mtrand.pyx, legacy): rounds of
@@ -229,13 +231,30 @@ class Work {
   // after = unique(concat(found, prev)), ascending; then the membership bitmap of `after`
   // with per-word rank prefixes (N/8 + N/16 bytes: L1/L2-resident, unlike an N-entry int32
   // map): the new column of c is rank[c / 64] + popcount(bits[c / 64] below bit c % 64).
-  void make_after(const std::vector<int64_t>& prev, std::vector<int64_t>& after) {
+  void make_after(const std::vector<int64_t>& prev, std::vector<int64_t>& after, bool columns = true) {
     after.assign(found.begin(), found.end());
     after.insert(after.end(), prev.begin(), prev.end());
     std::sort(after.begin(), after.end());
     after.erase(std::unique(after.begin(), after.end()), after.end());
     for (int64_t v : found) taken[(size_t)v] = 0;
-    set_columns(after);
+    if (columns) set_columns(after);
+  }
+
+  // A layer left to the GPU extraction: its rows and columns as int32 node ids, and from the
+  // column counts of U (structural: data == NULL) the exact nnz of U[:, after] and its CSC
+  // column pointer — colptr[j + 1] - colptr[j] = count of U's column after[j].
+  void device_layer(const std::vector<int64_t>& prev, const std::vector<int64_t>& after, Layer& L) const {
+    L.on_device = true;
+    L.rows.assign(prev.begin(), prev.end());
+    L.cols.assign(after.begin(), after.end());
+    L.colptr.resize(after.size() + 1);
+    int64_t acc = 0;
+    L.colptr[0] = 0;
+    for (size_t j = 0; j < after.size(); ++j) {
+      acc += cnt[(size_t)after[j]];
+      L.colptr[j + 1] = (int32_t)acc;
+    }
+    L.nnz = acc;
   }
 
   void set_columns(const std::vector<int64_t>& cols) {
@@ -271,6 +290,7 @@ class Work {
       L.rowptr[r + 1] = (int32_t)(w - base);
     }
     L.colidx.assign(base, w);
+    L.nnz = (int64_t)L.colidx.size();
   }
 
   // normfact = 1 / float32(clip(s_num * p[cols], 1e-10, 1))  (sampler.py:137: float32 division)
@@ -348,9 +368,19 @@ int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out) {
 int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
+  return gnn_ladies_sample_dev(indptr, indices, data, num_nodes, batch_nodes, batch_size, samp_num, orders,
+                               num_layers, seed, 0, out);
+}
+
+int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                          const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                          const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
+                          gnn_ladies_result** out) {
   if (int rc = check_inputs("gnn_ladies_sample", indptr, indices, num_nodes, batch_nodes, batch_size, samp_num,
                             orders, num_layers, out))
     return rc;
+  if (device_extract && data)
+    return fail("gnn_ladies_sample_dev: device extraction needs a graph without stored zeros (data == NULL)");
   *out = nullptr;
   try {
     const Graph g{indptr, indices, data, (size_t)num_nodes};
@@ -367,10 +397,13 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
       w.in_prev[(size_t)v] = 1;
     }
     for (int64_t v : prev) w.in_prev[(size_t)v] = 0;
+    bool top = true;  // the first sampled layer: its rows are the batch (any order, repeats)
     for (int32_t d = 0; d < num_layers; ++d) {
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
       if (orders[num_layers - 1 - d] == 0) continue;         // orders1 = orders[::-1]
       L.present = true;
+      const bool dev = device_extract && !top;  // rows = np.unique(...) of the layer above
+      top = false;
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
       if (unnz < 0) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
       // p = pi / sum(pi): exact integer sum
@@ -381,8 +414,13 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
       const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[d]);
       L.s_num = s_num;
       choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
-      w.make_after(prev, after);
-      w.extract(prev, unnz, L);
+      w.make_after(prev, after, !dev);
+      if (dev) {
+        w.device_layer(prev, after, L);
+        if (L.nnz >= ((int64_t)1 << 31)) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
+      } else {
+        w.extract(prev, unnz, L);
+      }
       w.normfact(after, total, s_num, L);
       w.positions(after, prev, L);
       L.M = (int64_t)prev.size();
@@ -518,7 +556,7 @@ int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dim
   const Layer& L = r->layers[(size_t)layer];
   dims[0] = L.M;
   dims[1] = L.K;
-  dims[2] = (int64_t)L.colidx.size();
+  dims[2] = L.nnz;
   dims[3] = (int64_t)L.sampled.size();
   dims[4] = L.s_num;
   return L.present ? 0 : 1;
@@ -531,6 +569,7 @@ int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fu
   auto cp = [](void* dst, const void* src, size_t bytes) {
     if (dst && bytes) std::memcpy(dst, src, bytes);
   };
+  // (on_device layers: fullrowptr / rowptr / colidx are not made; nothing is copied for them)
   cp(fullrowptr, L.fullrowptr.data(), L.fullrowptr.size() * 4);
   cp(rowptr, L.rowptr.data(), L.rowptr.size() * 4);
   cp(colidx, L.colidx.data(), L.colidx.size() * 4);
@@ -539,10 +578,22 @@ int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fu
   return 0;
 }
 
+int gnn_ladies_layer_device(const gnn_ladies_result* r, int32_t layer, int32_t* rows, int32_t* cols,
+                            int32_t* colptr) {
+  if (!r || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_device: bad args");
+  const Layer& L = r->layers[(size_t)layer];
+  if (!L.present || !L.on_device) return 1;
+  if (rows && !L.rows.empty()) std::memcpy(rows, L.rows.data(), L.rows.size() * 4);
+  if (cols && !L.cols.empty()) std::memcpy(cols, L.cols.data(), L.cols.size() * 4);
+  if (colptr) std::memcpy(colptr, L.colptr.data(), L.colptr.size() * 4);
+  return 0;
+}
+
 int gnn_ladies_layer_csc(const gnn_ladies_result* r, int32_t layer, int32_t* colptr, int32_t* rows) {
   if (!r || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_csc: bad args");
   const Layer& L = r->layers[(size_t)layer];
   if (!L.present) return fail("gnn_ladies_layer_csc: layer %d has no sub-graph", layer);
+  if (L.on_device) return fail("gnn_ladies_layer_csc: layer %d is extracted on the device", layer);
   if (!colptr || (!rows && !L.colidx.empty())) return fail("gnn_ladies_layer_csc: NULL output");
   // stable counting sort of the entries by column: rows come out ascending in each column
   std::fill(colptr, colptr + L.K + 1, 0);

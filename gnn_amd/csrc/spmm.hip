@@ -1259,6 +1259,12 @@ int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hi
 
 }  // namespace
 
+int gnn::launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st) {
+  scan_exclusive_kernel<<<dim3(1), dim3(1024), 0, st>>>(in, n, out, nullptr);
+  GNN_LAUNCHED("scan_exclusive_kernel");
+  return 0;
+}
+
 // =================================================================================
 // C ABI
 // =================================================================================

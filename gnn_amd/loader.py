@@ -77,12 +77,15 @@ class BatchLoader:
     def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
-                 seed: int = 0, devices=None, kind: str = "ladies"):
+                 seed: int = 0, devices=None, kind: str = "ladies", device_extract: bool = False):
         fns = {"ladies": smp.ladies_sample_host, "subgraph": smp.subgraph_sample_host,
                "fastgcn": smp.fastgcn_sample_host}
         if kind not in fns:
             raise ValueError("sampler configuration is wrong")  # main.py:88
         self.sample_fn = fns[kind]
+        # LADIES: leave the layers below the top one to the GPU extraction (to_device), so the
+        # worker threads only draw (sampler.ladies_sample_host(device_extract=True))
+        self.kw = {"device_extract": True} if device_extract and kind == "ladies" else {}
         self.graph = smp.native_graph(lap)
         self.labels = labels_full
         self.train = np.asarray(train_nodes)
@@ -102,7 +105,7 @@ class BatchLoader:
 
     def _produce(self, seed: int, nodes: np.ndarray) -> LoadedBatch:
         hb = self.sample_fn(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels, self.orders,
-                            self.dev_of, self.idx_on, None, 1.0, self.devices)
+                            self.dev_of, self.idx_on, None, 1.0, self.devices, **self.kw)
         hb.pin()
         plan = staging.make_plan(hb, self.store, self.rank, self.world, self.devices) if self.store else None
         return LoadedBatch(hb, plan)

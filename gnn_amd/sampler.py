@@ -26,13 +26,27 @@ import torch
 
 @dataclass
 class HostLayer:
-    fullrowptr: np.ndarray  # int32 [M+1]: indptr of U = lap[previous, :]
-    rowptr: np.ndarray      # int32 [M+1]: indptr of U[:, after]
-    colidx: np.ndarray      # int32 [nnz]
+    fullrowptr: Optional[np.ndarray]  # int32 [M+1]: indptr of U = lap[previous, :]
+    rowptr: Optional[np.ndarray]      # int32 [M+1]: indptr of U[:, after]
+    colidx: Optional[np.ndarray]      # int32 [nnz]
     normfact: np.ndarray    # float32 [K]: 1 / float32(clip(s_num * p[after], 1e-10, 1))
     shape: tuple            # (M, K)
     csc_colptr: Optional[np.ndarray] = None  # int32 [K+1]: CSC of the sub-graph (= CSR of its
     csc_rows: Optional[np.ndarray] = None    # transpose, rows ascending per column), if made
+    # A layer left to the GPU extraction (gnn_ladies_extract_f32): fullrowptr / rowptr / colidx
+    # are None; rows = U's rows (node ids, ascending), cols = after_nodes, csc_colptr from the
+    # column counts, dev_nnz = its exact nnz.
+    rows: Optional[np.ndarray] = None
+    cols: Optional[np.ndarray] = None
+    dev_nnz: int = -1
+
+    @property
+    def on_device(self) -> bool:
+        return self.colidx is None and self.rows is not None
+
+    @property
+    def nnz(self) -> int:
+        return int(self.dev_nnz) if self.on_device else int(self.colidx.size)
 
 
 @dataclass
@@ -54,7 +68,7 @@ class HostBatch:
         return int(len(self.input_nodes))
 
     def nnz(self) -> int:
-        return int(sum(l.colidx.size for l in self.layers if l is not None))
+        return int(sum(l.nnz for l in self.layers if l is not None))
 
     def pin(self) -> "HostBatch":
         """Copy the arrays the GPU needs into pinned host tensors (done by the batch producer
@@ -62,11 +76,10 @@ class HostBatch:
         if "pinned" not in self.extra:
             pin = torch.cuda.is_available()
             t = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dtype=dt))
-            p = lambda x: x.pin_memory() if pin else x
+            p = lambda x: None if x is None else (t(x).pin_memory() if pin else t(x))
             layers = [None if L is None else
-                      (p(t(L.fullrowptr)), p(t(L.rowptr)), p(t(L.colidx)), p(t(L.normfact)),
-                       None if L.csc_colptr is None else p(t(L.csc_colptr)),
-                       None if L.csc_rows is None else p(t(L.csc_rows)))
+                      (p(L.fullrowptr), p(L.rowptr), p(L.colidx), p(L.normfact), p(L.csc_colptr), p(L.csc_rows),
+                       p(L.rows), p(L.cols))
                       for L in self.layers]
             sampled = [p(t(s, np.int64)) for s in self.sampled_nodes]
             self.extra["pinned"] = (layers, sampled, p(t(self.labels)))
@@ -104,19 +117,25 @@ class HostBatch:
         sampled = [torch.from_numpy(np.asarray(s, dtype=np.int64)) for s in self.sampled_nodes]
         return adjs, x0, sampled, torch.from_numpy(self.labels)
 
-    def to_device(self, device, with_coo: bool = True, build: bool = True):
-        """Materialise on the GPU (H2D of the CSR pieces, labels, sampled_nodes) and, unless
-        build=False, run the operand builder. Returns a DeviceBatch."""
+    def to_device(self, device, with_coo: bool = True, build: bool = True, graph: "Optional[DeviceGraph]" = None):
+        """Materialise on the GPU (H2D of the CSR pieces — or, for layers left to the GPU
+        extraction, of their rows / columns / CSC column pointer — labels, sampled_nodes) and,
+        unless build=False, run the operand builder / extraction. Returns a DeviceBatch.
+        ``graph``: the graph resident on the device (default: device_graph() of the batch's
+        sampler graph), needed only by GPU-extracted layers."""
         dev = torch.device(device)
         layers, sampled, labels = self.pin().extra["pinned"]
         d = lambda x: None if x is None else x.to(dev, non_blocking=True)
-        raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape, d(P[4]), d(P[5]))
+        raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape, d(P[4]), d(P[5]), d(P[6]),
+                                       d(P[7]), L.nnz)
                for P, L in zip(layers, self.layers)]
         sn = [d(s) for s in sampled]
         for x, r in zip(sn, self.extra["rmaps"]):
             if r is not None:
                 x._gnn_rmap = d(r)  # read by fused.SageAggregateFn's backward
-        db = DeviceBatch(self, raw, None, sn, d(labels))
+        if graph is None and any(L is not None and L.on_device for L in self.layers):
+            graph = device_graph(self.extra["graph"], dev)
+        db = DeviceBatch(self, raw, None, sn, d(labels), graph)
         if build:
             db.build_operands(with_coo=with_coo)
         return db
@@ -126,15 +145,17 @@ class HostBatch:
 class DeviceBatch:
     host: HostBatch
     raw: list            # per layer: device (fullrowptr, rowptr, colidx, normfact, shape, csc_colptr|None,
-                         # csc_rows|None) or None
+                         # csc_rows|None, rows|None, cols|None, nnz) or None
     adjs: Optional[list]
     sampled_nodes: list
     labels: torch.Tensor
+    graph: Optional["DeviceGraph"] = None
 
     def tensors(self) -> list:
         """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
         maps), labels and the built operands (record_stream across streams)."""
-        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6]) if t is not None]
+        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6], r[7], r[8])
+              if t is not None]
         for x in self.sampled_nodes:
             ts.append(x)
             if getattr(x, "_gnn_rmap", None) is not None:
@@ -150,15 +171,21 @@ class DeviceBatch:
         from . import custom_sparse_ops as cso
 
         adjs = []
-        for r in self.raw:
+        csc_from = int(self.host.extra.get("csc_from", 1))
+        for li, r in enumerate(self.raw):
             if r is None:
                 adjs.append(None)
                 continue
-            fr, rp, ci, nf, shape, cp, cr = r
-            op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo,
-                                        sorted_rows=bool(self.host.extra.get("sorted_rows", False)))
-            if cp is not None:  # host-made CSC: the backward's operand without a GPU transpose
-                cso.attach_transpose(op, fr, cp, cr, nf)
+            fr, rp, ci, nf, shape, cp, cr, rows, cols, nnz = r
+            if ci is None:  # left to the GPU extraction (rows / cols / column counts from the draw)
+                _require_graph(self.graph)
+                op = cso.extract_operand(self.graph, rows, cols, nf, nnz, cp if li >= csc_from else None)
+                coo = op.to_torch_coo()._indices() if with_coo else None
+            else:
+                op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo,
+                                            sorted_rows=bool(self.host.extra.get("sorted_rows", False)))
+                if cp is not None:  # host-made CSC: the backward's operand without a GPU transpose
+                    cso.attach_transpose(op, fr, cp, cr, nf)
             if with_coo:
                 a = torch.sparse_coo_tensor(coo, op.val, shape, is_coalesced=True)
                 a._gnn_csr = op
@@ -167,6 +194,62 @@ class DeviceBatch:
                 adjs.append(op)
         self.adjs = adjs
         return adjs
+
+
+def _require_graph(graph) -> None:
+    if graph is None:
+        raise RuntimeError("a GPU-extracted layer needs the graph on the device (DeviceGraph)")
+
+
+class DeviceGraph:
+    """A NativeGraph's structure resident in device memory for gnn_ladies_extract_f32: canonical
+    CSR of lap (int64 indptr, int32 indices) and of lapᵀ (the same arrays when the structure is
+    symmetric), one node map per stream (int32[N], -1 between calls) and an error flag the
+    extraction raises if a device count disagrees with the host's."""
+
+    def __init__(self, graph: "NativeGraph", device):
+        dev = torch.device(device)
+        self.device = dev
+        self.num_nodes = graph.num_nodes
+        self.indptr = torch.from_numpy(graph.indptr).to(dev)
+        self.indices = torch.from_numpy(graph.indices).to(dev)
+        lt = graph.lap.T.tocsr()
+        lt.sum_duplicates()
+        lt.sort_indices()
+        self.symmetric = bool(np.array_equal(lt.indptr, graph.indptr) and np.array_equal(lt.indices, graph.indices))
+        if self.symmetric:
+            self.indptr_t, self.indices_t = self.indptr, self.indices
+        else:
+            self.indptr_t = torch.from_numpy(np.ascontiguousarray(lt.indptr, dtype=np.int64)).to(dev)
+            self.indices_t = torch.from_numpy(np.ascontiguousarray(lt.indices, dtype=np.int32)).to(dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._maps = {}
+
+    def node_map(self, stream: int) -> torch.Tensor:
+        """The node map of `stream` (created on first use, on the current stream = `stream`)."""
+        m = self._maps.get(stream)
+        if m is None:
+            m = torch.full((self.num_nodes,), -1, dtype=torch.int32, device=self.device)
+            self._maps[stream] = m
+        return m
+
+    def check(self) -> None:
+        """Raise if any extraction so far saw a count that disagrees with the host's (syncs)."""
+        e = int(self.err.item())
+        if e:
+            raise RuntimeError(f"gnn_ladies_extract_f32: device counts disagree with the host's (flag {e})")
+
+
+def device_graph(graph, device) -> DeviceGraph:
+    """The DeviceGraph of a NativeGraph (or lap matrix) on `device`, made once and cached."""
+    g = native_graph(graph)
+    dev = torch.device(device)
+    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
+    dg = g._device_graphs.get(key)
+    if dg is None:
+        dg = DeviceGraph(g, dev)
+        g._device_graphs[key] = dg
+    return dg
 
 
 def column_nnz_counts(U: sp.csr_matrix, num_nodes: int) -> np.ndarray:
@@ -197,6 +280,7 @@ class NativeGraph:
         self.data = None if np.all(data != 0) else np.ascontiguousarray(data, dtype=np.float32)
         self.lap = lap
         self._fastgcn_p = None
+        self._device_graphs = {}
 
     @property
     def fastgcn_p(self) -> np.ndarray:
@@ -220,10 +304,12 @@ def native_graph(lap) -> NativeGraph:
 
 
 def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies",
-                   csc_from: int = 1):
+                   csc_from: int = 1, device_extract: bool = False):
     """Run gnn_ladies_sample / gnn_subgraph_sample / gnn_fastgcn_sample and copy the result
     out: (layers, sampled_nodes, input_nodes, pinned tensors). Layers >= csc_from (those
-    whose input needs a gradient; layer 0's input is the features) also get their CSC."""
+    whose input needs a gradient; layer 0's input is the features) also get their CSC.
+    device_extract (LADIES): the layers below the top one are left to the GPU extraction —
+    only their rows, columns, CSC column pointer and nnz come back."""
     import ctypes
 
     from . import _lib
@@ -239,6 +325,8 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
     rest = (ptr(bn), bn.size, ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF, ctypes.byref(h))
     if kind == "fastgcn":
         rc = L.gnn_fastgcn_sample(*g3, ptr(graph.fastgcn_p), *rest)
+    elif kind == "ladies" and device_extract:
+        rc = L.gnn_ladies_sample_dev(*g3, *rest[:-1], 1, rest[-1])
     else:
         rc = (L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample)(*g3, *rest)
     _lib.check_sampler(rc, f"gnn_{kind}_sample")
@@ -264,12 +352,24 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
                 pinned_sampled.append(buf(0, torch.int64)[0])
                 continue
             M, K, nnz, ns = dims[0], dims[1], dims[2], dims[3]
-            (tfr, fr), (trp, rp), (tci, ci) = buf(M + 1, torch.int32), buf(M + 1, torch.int32), buf(nnz, torch.int32)
             (tnf, nf), (tsa, sa) = buf(K, torch.float32), buf(ns, torch.int64)
+            if device_extract and L.gnn_ladies_layer_device(h, li, None, None, None) == 0:
+                (trw, rw), (tcl, cl), (tcp, cp) = buf(M, torch.int32), buf(K, torch.int32), buf(K + 1, torch.int32)
+                _lib.check_sampler(L.gnn_ladies_layer_device(h, li, ptr(rw), ptr(cl), ptr(cp)) & ~1,
+                                   "gnn_ladies_layer_device")
+                _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, None, None, None, ptr(nf), ptr(sa)),
+                                   "gnn_ladies_layer_copy")
+                pinned_layers.append((None, None, None, tnf, tcp, None, trw, tcl))
+                pinned_sampled.append(tsa)
+                layers.append(HostLayer(fullrowptr=None, rowptr=None, colidx=None, normfact=nf, shape=(int(M), int(K)),
+                                        csc_colptr=cp, rows=rw, cols=cl, dev_nnz=int(nnz)))
+                sampled.append(sa)
+                continue
+            (tfr, fr), (trp, rp), (tci, ci) = buf(M + 1, torch.int32), buf(M + 1, torch.int32), buf(nnz, torch.int32)
             tcp = tcr = cp = cr = None
             if li >= csc_from:  # layers whose input needs a gradient: the backward's operand
                 (tcp, cp), (tcr, cr) = buf(K + 1, torch.int32), buf(nnz, torch.int32)
-            pinned_layers.append((tfr, trp, tci, tnf, tcp, tcr))
+            pinned_layers.append((tfr, trp, tci, tnf, tcp, tcr, None, None))
             pinned_sampled.append(tsa)
             _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, ptr(fr), ptr(rp), ptr(ci), ptr(nf), ptr(sa)),
                                "gnn_ladies_layer_copy")
@@ -288,24 +388,28 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
 def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
                        orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
                        skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
-                       native: bool = True) -> HostBatch:
+                       native: bool = True, device_extract: bool = False) -> HostBatch:
     """sampler.py:90-160 without the device work.
 
     native=True runs the C++ sampler (libgnn_sampler.so, bit-identical; releases the GIL, so
     batches sample concurrently on threads); native=False (and scale_factor > 1, a branch the
-    reference never reaches) runs the numpy restatement below."""
+    reference never reaches) runs the numpy restatement below. device_extract=True (native, a
+    graph without stored zeros): the layers below the top one are extracted on the GPU by
+    ``to_device`` (gnn_ladies_extract_f32) instead of on the host — same operands."""
     batch_nodes = np.asarray(batch_nodes)
     if native and not scale_factor > 1:
         g = native_graph(lap_matrix)
         if g.num_nodes != num_nodes:
             raise ValueError("num_nodes does not match lap_matrix")
+        dx = bool(device_extract) and g.data is None
         layers, sampled_nodes, previous_nodes, pinned = _native_layers(seed, batch_nodes, samp_num_list, g,
-                                                                       list(orders))
+                                                                       list(orders), device_extract=dx)
         hb = _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,
                            idx_of_nodes_on_device, devices, seed)
         lab = torch.from_numpy(hb.labels)
         hb.extra["pinned"] = (pinned[0], pinned[1], lab.pin_memory() if torch.cuda.is_available() else lab)
         hb.extra["sorted_rows"] = True  # native samplers emit column-ascending rows by construction
+        hb.extra["graph"] = g
         return hb
     if isinstance(lap_matrix, NativeGraph):
         lap_matrix = lap_matrix.lap

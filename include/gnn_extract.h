@@ -1,0 +1,56 @@
+/* gnn_extract.h — C ABI of the GPU-side LADIES layer extraction (libgnn_spmm.so, gfx950).
+ *
+ * Replaces, for every sampled layer whose rows are unique and ascending (all layers below the
+ * top one: their rows are the np.unique output of the layer above), the host half of
+ *   reference sampler.py:114   U = lap_matrix[previous_nodes, :]
+ *   reference sampler.py:133   adj = U[:, after_nodes]
+ *   reference sampler.py:135-139  rowptr / colidx / normfact -> create_coo_tensor
+ * and the device half, create_coo_tensor (spmm_cpp/spmm.cpp:44-50 -> cuda_spmm.cu:787-827),
+ * in one stream-ordered call that reads the graph's CSR resident in device memory. The host
+ * sampler keeps the draw (np.random.choice over the column counts of U) and hands over the rows
+ * (previous_nodes), the columns (after_nodes), normfact, and — from the same column counts —
+ * the exact nnz and the CSC column pointer of adj.
+ *
+ * Conventions as gnn_spmm.h: device pointers, a hipStream_t as void*, no host syncs, no
+ * allocation (graph-capturable), 0 on success / negative or hipError_t code with the message in
+ * gnn_last_error().
+ */
+#ifndef GNN_EXTRACT_H
+#define GNN_EXTRACT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The operand of one sampled layer and, optionally, its transpose.
+ *
+ * Graph (device): the lap matrix as canonical CSR (indptr int64[num_nodes+1], indices int32,
+ * columns ascending per row, no duplicates); indptr_t / indices_t: the same for lap^T (may alias
+ * indptr / indices when the structure is symmetric). deg(v) = indptr[v+1] - indptr[v].
+ * rows  int32[M]: U's rows (node ids) in order; cols int32[K]: after_nodes, strictly ascending;
+ * normfact fp32[K]; nnz = number of entries of U[:, cols] (the sum of U's column counts over cols).
+ * node_map int32[num_nodes]: workspace, every entry -1 on entry, restored to -1 (stream order);
+ * one map per stream. rowcnt int32[M]: workspace.
+ * Outputs: rowptr int32[M+1], col int32[nnz] (positions into cols, ascending per row),
+ * val fp32[nnz] = (float)((1.0 / deg(rows[i])) * (double)normfact[col]) — identical to
+ * gnn_build_operand_f32 on the host-extracted pieces with fullrowptr = the rows' degrees.
+ * Transpose (colptr_t != NULL; rows must then be unique and ascending): colptr_t int32[K+1] is
+ * the CSC column pointer (host-known: the column counts), rows_t int32[nnz] / val_t fp32[nnz]
+ * receive the canonical CSR of adj^T (rows ascending in each column) — what
+ * gnn_csr_transpose / A.t().coalesce() would produce.
+ * err_flag (device int32, optional): OR-ed with 1 if the device row counts do not add up to nnz,
+ * 2 if a column's count differs from colptr_t (writes stay clamped inside their segments). */
+int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, int64_t num_nodes, const int64_t* indptr_t,
+                           const int32_t* indices_t, const int32_t* rows, int64_t M, const int32_t* cols, int64_t K,
+                           const float* normfact, int64_t nnz, const int32_t* colptr_t, int32_t* node_map,
+                           int32_t* rowptr, int32_t* col, float* val, int32_t* rowcnt, int32_t* rows_t, float* val_t,
+                           int32_t* err_flag, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNN_EXTRACT_H */

@@ -41,6 +41,18 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
 
+/* Same draw (bit-identical RNG stream, sampled nodes, normfact), with device_extract != 0: every
+ * layer below the top one (its rows are the ascending, unique `after` of the layer above) is NOT
+ * extracted on the host — the host keeps only what the draw needs (U's column counts) and records
+ * the layer's rows, columns, exact nnz and CSC column pointer for gnn_ladies_extract_f32
+ * (include/gnn_extract.h), which builds adj = U[:, after] and its transpose on the GPU from the
+ * graph resident there. Requires data == NULL (no stored zeros: the column counts are then the
+ * structural counts the extraction keeps). The top layer (rows = the batch) is host-extracted. */
+int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                          const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                          const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
+                          gnn_ladies_result** out);
+
 /* subgraph_sampler (sampler.py:7-88): ONE importance draw from the batch's neighbourhood
  * (same p, s_num = min(#(p > 0), samp_num[0]), same RNG use), after = unique(sampled ∪ batch);
  * the top-most layer with a non-zero order gets lap[batch, :][:, after]; every layer below it
@@ -70,6 +82,14 @@ int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dim
  * pointer may be NULL to skip that array. */
 int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fullrowptr, int32_t* rowptr,
                           int32_t* colidx, float* normfact, int64_t* sampled);
+
+/* A layer left to the device extraction: rows int32[M] (U's rows, node ids), cols int32[K]
+ * (after_nodes, ascending), colptr int32[K+1] (CSC column pointer of adj; colptr[K] = nnz).
+ * Returns 0 and copies (NULL pointers skip) for such a layer, 1 for a host-extracted or absent
+ * layer (nothing copied). fullrowptr / rowptr / colidx of gnn_ladies_layer_copy are not made for
+ * it; normfact and sampled are. */
+int gnn_ladies_layer_device(const gnn_ladies_result* r, int32_t layer, int32_t* rows, int32_t* cols,
+                            int32_t* colptr);
 
 /* CSC structure of layer `layer`'s sub-graph (= CSR of its transpose, canonical: rows
  * ascending inside each column): colptr int32[K+1], rows int32[nnz]. Lets the training
