@@ -91,6 +91,9 @@ def parse():
     ap.add_argument("--host-extract", action="store_true",
                     help="LADIES: extract every layer's sub-graph on the host (sampler threads) instead of "
                          "leaving the layers below the top one to the GPU extraction (gnn_ladies_extract_f32)")
+    ap.add_argument("--python-loader", action="store_true",
+                    help="batch producer: Python worker threads calling the native sampler (BatchLoader) instead of "
+                         "the C++ producer (NativeLoader: GIL-free workers, one blob and one H2D per batch)")
     ap.add_argument("--cprofile", default="", help="after the timed runs, cProfile 20 GPU steps into this file")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     a = ap.parse_args()
@@ -503,13 +506,13 @@ def main():
         return el, issued, out
 
     # ------------------------------------------------- headline: end to end, live sampling
-    from gnn_amd.loader import BatchLoader
+    from gnn_amd.loader import BatchLoader, NativeLoader
 
     workers = args.workers or default_workers(world)
     dx = args.sampler == "ladies" and not args.host_extract
-    loader = BatchLoader(lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank,
-                         world_size=world, store=store, workers=workers, seed=4242, kind=args.sampler,
-                         device_extract=dx)
+    loader = (BatchLoader if args.python_loader else NativeLoader)(
+        lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank, world_size=world,
+        store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx)
     if dx:  # the graph resident in HBM for the extraction (made once, outside every timed region)
         sampler.device_graph(loader.graph, dev)
         torch.cuda.synchronize()
@@ -533,15 +536,26 @@ def main():
         nwarm = max(2, min(args.warmup, 10))
         pre = [next(it) for _ in range(nwarm + args.steps)]
         loader.close()
-        # CSR pieces, labels and index arrays resident in HBM; the operand builder (the
-        # create_coo_tensor kernel) runs for every step, on the staging stream ahead of it
-        dbs = [lb.host.to_device(dev, build=False) for lb in pre]
+        native = not args.python_loader
+        if native:
+            # the batch blobs (CSR pieces or GPU-extraction inputs, labels, index arrays, host
+            # rows) are uploaded in the timed region, one H2D each, as the live run does
+            dbs = [None] * len(pre)
+        else:
+            # CSR pieces, labels and index arrays resident in HBM; the operand builder (the
+            # create_coo_tensor kernel) runs for every step, on the staging stream ahead of it
+            dbs = [lb.host.to_device(dev, build=False) for lb in pre]
         torch.cuda.synchronize()
         k_ = [0]
 
         def nxt_pre():
             j = k_[0]
             k_[0] += 1
+            if native:
+                def fn(j=j):
+                    dbs[j] = pre[j].host.to_device(dev, with_coo=False)
+                    return dbs[j]
+                return pre[j].plan, fn
             db = dbs[j]
             return pre[j].plan, lambda: (db.build_operands(), db)[1]
 
@@ -555,8 +569,11 @@ def main():
         gpu_step = {"value": round(world * args.steps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / args.steps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / args.steps, 3),
-                    "what": f"{args.steps} distinct pre-sampled batches per rank (none cycled), CSR pieces resident "
-                            "in HBM; X0 staging, operand builds and the whole training step inside the timed region"}
+                    "what": f"{args.steps} distinct pre-sampled batches per rank (none cycled); "
+                            + ("each batch's blob upload (one H2D), X0 staging, GPU layer extraction / operand builds "
+                               "and the whole training step inside the timed region" if native else
+                               "CSR pieces resident in HBM; X0 staging, operand builds and the whole training step "
+                               "inside the timed region")}
         staging_info = {"mode": args.staging, "host_rows_MB_per_batch": round(h_bytes / args.steps / 1e6, 2),
                         "h2d_GBps": round(h_bytes / h_sec / 1e9, 1) if h_sec > 0 else None,
                         "h2d_ms_per_batch": round(1e3 * h_sec / args.steps, 3),
@@ -630,6 +647,7 @@ def main():
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
                        "sampler_workers_per_rank": workers,
+                       "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
                        "layer_extraction": "gpu (layers below the top one)" if dx else "host"},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -48,6 +48,7 @@ _SIGNATURES = {
     "gnn_gather_rows_host_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
     "gnn_host_register": (_INT, [_VP, _SZ]),
     "gnn_host_unregister": (_INT, [_VP]),
+    "gnn_memcpy_h2d_async": (_INT, [_VP, _VP, _SZ, _VP]),
     # include/gnn_layers.h
     "gnn_sage_norm_fwd_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _I64, ctypes.c_float,
                                      ctypes.c_uint64, _INT, _VP, _I64, _VP, _VP, _VP]),
@@ -99,6 +100,15 @@ _SAMPLER_SIGNATURES = {
     "gnn_ladies_free": (None, [_VP]),
     "gnn_mt19937_random_sample": (_INT, [ctypes.c_uint32, _I64, _VP]),
     "gnn_host_gather_rows_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _I64]),
+    "gnn_loader_create": (_VP, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32,
+                                _VP, _VP, _I64, _I64, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32, _VP,
+                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "gnn_loader_submit": (_INT, [_VP, ctypes.c_uint32, _VP, _I64]),
+    "gnn_loader_next": (_INT, [_VP, ctypes.POINTER(_VP)]),
+    "gnn_batch_desc": (ctypes.POINTER(_I64), [_VP, ctypes.POINTER(_I64)]),
+    "gnn_batch_blob": (_VP, [_VP]),
+    "gnn_batch_release": (None, [_VP]),
+    "gnn_loader_destroy": (None, [_VP]),
 }
 SAMPLER_EXPORTED_SYMBOLS = tuple(_SAMPLER_SIGNATURES)
 _sampler = None

@@ -43,8 +43,8 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
-SAMPLER_SRCS = [os.path.join(HERE, "csrc", "sampler.cpp")]
-SAMPLER_HDRS = [os.path.join(REPO, "include", "gnn_sampler.h")]
+SAMPLER_SRCS = [os.path.join(HERE, "csrc", f) for f in ("sampler.cpp", "loader.cpp")]
+SAMPLER_HDRS = [os.path.join(REPO, "include", "gnn_sampler.h"), os.path.join(HERE, "csrc", "sampler_internal.h")]
 SAMPLER_OUT = os.path.join(HERE, "libgnn_sampler.so")
 
 
@@ -61,7 +61,7 @@ def build_sampler(force: bool = False, verbose: bool = False) -> str:
                 return SAMPLER_OUT
     # x86-64-v2 (SSE4.2 + POPCNT), not -march=native: the GPU box's host CPU may differ
     cmd = [os.environ.get("CXX", "g++"), "-O3", "-march=x86-64-v2", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           f"-I{os.path.join(REPO, 'include')}", "-o", SAMPLER_OUT + ".tmp"] + SAMPLER_SRCS
+           f"-I{os.path.join(REPO, 'include')}", "-pthread", "-o", SAMPLER_OUT + ".tmp"] + SAMPLER_SRCS + ["-ldl"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -6,6 +6,7 @@
 // rows plus O(#nonzero columns) work per choice round, on scratch arrays owned by the call —
 // so batches sample concurrently on host threads (ctypes releases the GIL).
 #include "gnn_sampler.h"
+#include "sampler_internal.h"
 
 #include <algorithm>
 #include <cstdarg>
@@ -15,6 +16,8 @@
 #include <new>
 #include <string>
 #include <vector>
+
+using gnn_smp::Layer;
 
 namespace {
 
@@ -78,15 +81,6 @@ class MT19937 {
   int pos_;
 };
 
-struct Layer {
-  bool present = false;
-  bool on_device = false;  // entries left to the GPU extraction (gnn_ladies_extract_f32)
-  int64_t M = 0, K = 0, s_num = 0, nnz = 0;
-  std::vector<int32_t> fullrowptr, rowptr, colidx;
-  std::vector<float> normfact;
-  std::vector<int64_t> sampled;
-  std::vector<int32_t> rows, cols, colptr;  // on_device: U's rows, after_nodes, CSC column pointer
-};
 
 // RandomState.choice(N, size, p=p, replace=False) (numpy mtrand.pyx, legacy): rounds of
 // `rand(size - n_uniq)` draws, p of the already found entries zeroed, cdf = cumsum(p) /
@@ -349,10 +343,22 @@ int check_inputs(const char* who, const int64_t* indptr, const int32_t* indices,
 
 }  // namespace
 
-struct gnn_ladies_result {
-  std::vector<Layer> layers;  // bottom-up
-  std::vector<int64_t> input_nodes;
-};
+
+namespace gnn_smp {
+
+void layer_csc(const Layer& L, int32_t* colptr, int32_t* rows) {
+  // stable counting sort of the entries by column: rows come out ascending in each column
+  std::fill(colptr, colptr + L.K + 1, 0);
+  for (int32_t c : L.colidx) ++colptr[c + 1];
+  for (int64_t c = 0; c < L.K; ++c) colptr[c + 1] += colptr[c];
+  std::vector<int32_t> cur(colptr, colptr + L.K);
+  for (int64_t i = 0; i < L.M; ++i)
+    for (int32_t k = L.rowptr[(size_t)i]; k < L.rowptr[(size_t)i + 1]; ++k) rows[cur[(size_t)L.colidx[(size_t)k]]++] = (int32_t)i;
+}
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+}  // namespace gnn_smp
 
 extern "C" {
 
@@ -595,13 +601,7 @@ int gnn_ladies_layer_csc(const gnn_ladies_result* r, int32_t layer, int32_t* col
   if (!L.present) return fail("gnn_ladies_layer_csc: layer %d has no sub-graph", layer);
   if (L.on_device) return fail("gnn_ladies_layer_csc: layer %d is extracted on the device", layer);
   if (!colptr || (!rows && !L.colidx.empty())) return fail("gnn_ladies_layer_csc: NULL output");
-  // stable counting sort of the entries by column: rows come out ascending in each column
-  std::fill(colptr, colptr + L.K + 1, 0);
-  for (int32_t c : L.colidx) ++colptr[c + 1];
-  for (int64_t c = 0; c < L.K; ++c) colptr[c + 1] += colptr[c];
-  std::vector<int32_t> cur(colptr, colptr + L.K);
-  for (int64_t i = 0; i < L.M; ++i)
-    for (int32_t k = L.rowptr[(size_t)i]; k < L.rowptr[(size_t)i + 1]; ++k) rows[cur[(size_t)L.colidx[(size_t)k]]++] = (int32_t)i;
+  gnn_smp::layer_csc(L, colptr, rows);
   return 0;
 }
 

@@ -1583,6 +1583,13 @@ int gnn_host_unregister(void* host) {
   return 0;
 }
 
+int gnn_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes == 0) return 0;
+  GNN_REQUIRE(dst && src, "gnn_memcpy_h2d_async: NULL pointer");
+  GNN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream), "hipMemcpyAsync");
+  return 0;
+}
+
 int gnn_gather_rows_host_f32(const float* host_src, int64_t ld_src, const int64_t* src_idx, float* dst,
                              int64_t ld_dst, const int64_t* dst_idx, int64_t n, int64_t F, void* stream) {
   GNN_REQUIRE(n >= 0 && F >= 0, "gnn_gather_rows_host_f32: negative size");

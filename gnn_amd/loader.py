@@ -19,6 +19,7 @@ from dataclasses import dataclass
 from typing import Iterator, Optional, Sequence
 
 import numpy as np
+import torch
 
 from . import sampler as smp
 from . import staging
@@ -140,3 +141,299 @@ class BatchLoader:
 
     def close(self):
         self.pool.shutdown(wait=True, cancel_futures=True)
+
+
+# ----------------------------------------------------------------------------------------
+# Native batch producer (libgnn_sampler.so gnn_loader_*, include/gnn_sampler.h): the worker
+# threads are C++ and never take the GIL, so the training thread keeps the interpreter to itself;
+# each batch is ONE blob uploaded with ONE host-to-device copy.
+# ----------------------------------------------------------------------------------------
+# descriptor layout (mirrors GNN_BLOB_* / GNN_H_* / GNN_L_* / GNN_B_* of gnn_sampler.h)
+BLOB_VERSION, BLOB_HEADER, BLOB_LAYER_SLOTS, BLOB_BATCH_SLOTS = 1, 16, 32, 16
+H_VERSION, H_LAYERS, H_BYTES, H_BATCH, H_CLASSES, H_INPUTS, H_WORLD, H_LD_X0, H_SEED, H_PINNED = range(10)
+(L_PRESENT, L_ON_DEVICE, L_M, L_K, L_NNZ, L_SNUM, L_NSAMPLED, L_HAS_RMAP) = range(8)
+L_FULLROWPTR, L_ROWPTR, L_COLIDX, L_NORMFACT, L_CSC_COLPTR, L_CSC_ROWS, L_ROWS, L_COLS, L_SAMPLED, L_RMAP = \
+    range(8, 28, 2)
+B_LABELS, B_HOST_ROWS, B_OWN_POS, B_OWN_SRC, B_HOST_POS, B_HOST_SRC, B_INPUT_NODES = range(0, 14, 2)
+KINDS = {"ladies": 0, "subgraph": 1, "fastgcn": 2}
+_I32, _I64, _F32 = np.dtype(np.int32), np.dtype(np.int64), np.dtype(np.float32)
+_TDT = {_I32: torch.int32, _I64: torch.int64, _F32: torch.float32}
+
+
+class NativeBatch:
+    """One batch of the native loader: the host blob, its descriptor and views of its sections.
+
+    Duck-types the parts of ``sampler.HostBatch`` the training pipeline and the benchmark read
+    (``layers``, ``sampled_nodes``, ``input_nodes``, ``labels``, ``nnz()``, ``to_device``) and
+    carries the X0 staging plan (``plan``). The blob goes back to the loader's pool when this
+    object dies — after the step that read it (the staging path keeps it alive until then)."""
+
+    def __init__(self, handle: int, store: Optional[staging.FeatureStore]):
+        import ctypes
+        import weakref
+
+        from . import _lib
+
+        L = _lib.sampler_lib()
+        n = ctypes.c_int64()
+        dp = L.gnn_batch_desc(handle, ctypes.byref(n))
+        self.desc = np.ctypeslib.as_array(dp, shape=(n.value,)).copy()
+        self.nbytes = int(self.desc[H_BYTES])
+        self.ptr = int(L.gnn_batch_blob(handle))
+        self._release = weakref.finalize(self, L.gnn_batch_release, handle)
+        self.blob = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+        self.num_layers = int(self.desc[H_LAYERS])
+        self.world = int(self.desc[H_WORLD])
+        self.seed = int(self.desc[H_SEED])
+        self.pinned = bool(self.desc[H_PINNED])
+        self.extra = {"sorted_rows": True, "csc_from": 1}
+        self.store = store
+        self._dev = None  # (device, device blob) once uploaded
+        self._layers = None
+        bb = BLOB_HEADER + self.num_layers * BLOB_LAYER_SLOTS
+        self._bb = bb
+        self.input_nodes = self._h(bb + B_INPUT_NODES, _I64)
+        self.num_input_nodes = int(self.desc[H_INPUTS])
+        C = int(self.desc[H_CLASSES])
+        self.labels = self._h(bb + B_LABELS, _F32).reshape(-1, C) if C else np.zeros((0, 0), np.float32)
+        self.sampled_nodes = [self._h(self._lb(li) + L_SAMPLED, _I64) for li in range(self.num_layers)]
+        self.nodes_idx_on_cpu = self._h(bb + B_HOST_SRC, _I64)
+
+    # -- host views ------------------------------------------------------------------------
+    def _lb(self, li: int) -> int:
+        return BLOB_HEADER + li * BLOB_LAYER_SLOTS
+
+    def _count(self, slot: int) -> int:
+        return int(self.desc[slot + 1])
+
+    def _h(self, slot: int, dt: np.dtype) -> np.ndarray:
+        off, cnt = int(self.desc[slot]), int(self.desc[slot + 1])
+        return self.blob[off:off + cnt * dt.itemsize].view(dt)
+
+    @property
+    def layers(self) -> list:
+        if self._layers is None:
+            from .sampler import HostLayer
+
+            out = []
+            for li in range(self.num_layers):
+                b = self._lb(li)
+                if not self.desc[b + L_PRESENT]:
+                    out.append(None)
+                    continue
+                shape = (int(self.desc[b + L_M]), int(self.desc[b + L_K]))
+                if self.desc[b + L_ON_DEVICE]:
+                    out.append(HostLayer(fullrowptr=None, rowptr=None, colidx=None, normfact=self._h(b + L_NORMFACT, _F32),
+                                         shape=shape, csc_colptr=self._h(b + L_CSC_COLPTR, _I32),
+                                         rows=self._h(b + L_ROWS, _I32), cols=self._h(b + L_COLS, _I32),
+                                         dev_nnz=int(self.desc[b + L_NNZ])))
+                else:
+                    has_t = self._count(b + L_CSC_COLPTR) > 0
+                    out.append(HostLayer(fullrowptr=self._h(b + L_FULLROWPTR, _I32), rowptr=self._h(b + L_ROWPTR, _I32),
+                                         colidx=self._h(b + L_COLIDX, _I32), normfact=self._h(b + L_NORMFACT, _F32),
+                                         shape=shape, csc_colptr=self._h(b + L_CSC_COLPTR, _I32) if has_t else None,
+                                         csc_rows=self._h(b + L_CSC_ROWS, _I32) if has_t else None))
+            self._layers = out
+        return self._layers
+
+    def nnz(self) -> int:
+        return int(sum(self.desc[self._lb(li) + L_NNZ] for li in range(self.num_layers)
+                       if self.desc[self._lb(li) + L_PRESENT]))
+
+    @property
+    def plan(self) -> staging.StagePlan:
+        """The X0 staging plan (views of the blob). Made per access and not kept here: the plan
+        references this batch, and a cycle would hold the blob until the cyclic GC runs."""
+        bb = self._bb
+        W = self.world
+        peer_pos = [self._h(bb + BLOB_BATCH_SLOTS + 4 * j, _I64) for j in range(W)]
+        peer_src = [self._h(bb + BLOB_BATCH_SLOTS + 4 * j + 2, _I64) for j in range(W)]
+        return staging.StagePlan(self.num_input_nodes, self._h(bb + B_OWN_POS, _I64), self._h(bb + B_OWN_SRC, _I64),
+                                 self._h(bb + B_HOST_POS, _I64), None, peer_pos, peer_src, (), blob=self)
+
+    # -- device side -----------------------------------------------------------------------
+    def device_blob(self, dev) -> torch.Tensor:
+        """The blob on `dev`: one allocation + ONE host-to-device copy on the current stream
+        (made once; later calls return the same tensor)."""
+        from . import _lib
+
+        dev = torch.device(dev)
+        if self._dev is None or self._dev[0] != dev:
+            with _lib.on_device(dev):
+                d = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
+                _lib.check(_lib.lib().gnn_memcpy_h2d_async(d.data_ptr(), self.ptr, self.nbytes, _lib.stream_of(dev)),
+                           "gnn_memcpy_h2d_async")
+            self._dev = (dev, d)
+        return self._dev[1]
+
+    def _d(self, slot: int, dt: np.dtype) -> torch.Tensor:
+        off, cnt = int(self.desc[slot]), int(self.desc[slot + 1])
+        return self._dev[1][off:off + cnt * dt.itemsize].view(_TDT[dt])
+
+    def stage_views(self, dev):
+        """(own_pos, own_src, host_pos, host rows | host_src) on the device for Stager.issue."""
+        self.device_blob(dev)
+        bb = self._bb
+        ld = int(self.desc[H_LD_X0])
+        rows = self._d(bb + B_HOST_ROWS, _F32)
+        host = rows.view(-1, ld) if self._count(bb + B_HOST_ROWS) else self._d(bb + B_HOST_SRC, _I64)
+        return (self._d(bb + B_OWN_POS, _I64), self._d(bb + B_OWN_SRC, _I64), self._d(bb + B_HOST_POS, _I64), host)
+
+    def to_device(self, device, with_coo: bool = True, build: bool = True, graph=None):
+        """The DeviceBatch of this batch: views of the uploaded blob (no further copies), then
+        (build=True) the operand builds / GPU extractions on the current stream."""
+        from .sampler import DeviceBatch, device_graph
+
+        dev = torch.device(device)
+        self.device_blob(dev)
+        raw = []
+        for li in range(self.num_layers):
+            b = self._lb(li)
+            if not self.desc[b + L_PRESENT]:
+                raw.append(None)
+                continue
+            shape = (int(self.desc[b + L_M]), int(self.desc[b + L_K]))
+            if self.desc[b + L_ON_DEVICE]:
+                raw.append((None, None, None, self._d(b + L_NORMFACT, _F32), shape, self._d(b + L_CSC_COLPTR, _I32), None,
+                            self._d(b + L_ROWS, _I32), self._d(b + L_COLS, _I32), int(self.desc[b + L_NNZ])))
+            else:
+                has_t = self._count(b + L_CSC_COLPTR) > 0
+                raw.append((self._d(b + L_FULLROWPTR, _I32), self._d(b + L_ROWPTR, _I32), self._d(b + L_COLIDX, _I32),
+                            self._d(b + L_NORMFACT, _F32), shape, self._d(b + L_CSC_COLPTR, _I32) if has_t else None,
+                            self._d(b + L_CSC_ROWS, _I32) if has_t else None, None, None, int(self.desc[b + L_NNZ])))
+        sn = []
+        for li in range(self.num_layers):
+            b = self._lb(li)
+            x = self._d(b + L_SAMPLED, _I64)
+            if self.desc[b + L_PRESENT] and self.desc[b + L_HAS_RMAP]:
+                x._gnn_rmap = self._d(b + L_RMAP, _I32)  # read by fused.SageAggregateFn's backward
+            sn.append(x)
+        C = int(self.desc[H_CLASSES])
+        labels = self._d(self._bb + B_LABELS, _F32).view(-1, C)
+        if graph is None and any(self.desc[self._lb(li) + L_PRESENT] and self.desc[self._lb(li) + L_ON_DEVICE]
+                                 for li in range(self.num_layers)):
+            graph = device_graph(self.graph, dev)
+        db = DeviceBatch(self, raw, None, sn, labels, graph)
+        if build:
+            db.build_operands(with_coo=with_coo)
+        return db
+
+
+class NativeLoader:
+    """BatchLoader with C++ workers (gnn_loader_*): same batches (same seeds, same chunks,
+    same sampler calls), same ``epoch`` / ``forever`` interface, yielding LoadedBatch(host=
+    NativeBatch, plan=its StagePlan). ``store`` (copy mode) supplies the host feature table the
+    workers gather the non-buffered rows from; zero-copy stores leave the rows to the GPU."""
+
+    def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
+                 device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
+                 store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
+                 seed: int = 0, devices=None, kind: str = "ladies", device_extract: bool = False,
+                 pinned: Optional[bool] = None):
+        import scipy.sparse as sp
+
+        from . import _lib
+
+        if kind not in KINDS:
+            raise ValueError("sampler configuration is wrong")  # main.py:88
+        self.graph = smp.native_graph(lap)
+        g = self.graph
+        self.train = np.asarray(train_nodes)
+        self.batch_size = batch_size
+        self.rank, self.world = rank, world_size
+        self.store = store
+        self.workers = max(1, int(workers))
+        self.prefetch = prefetch if prefetch > 0 else 2 * self.workers
+        self.rng = np.random.RandomState(seed + 7919 * rank)
+        lab = sp.csr_matrix(labels_full)
+        nl = len(orders)
+        # borrowed by the C++ loader: kept alive here
+        self._keep = dict(
+            lab_ptr=np.ascontiguousarray(lab.indptr, dtype=np.int64),
+            lab_idx=np.ascontiguousarray(lab.indices, dtype=np.int32),
+            lab_val=np.ascontiguousarray(lab.data, dtype=np.float32),
+            dev_of=np.ascontiguousarray(device_id_of_nodes, dtype=np.int64),
+            idx_on=np.ascontiguousarray(idx_of_nodes_on_device, dtype=np.int64),
+            devices=np.ascontiguousarray(list(range(world_size)) if devices is None else list(devices), dtype=np.int64),
+            samp=np.ascontiguousarray([int(samp_num)] * nl, dtype=np.int64),
+            orders=np.ascontiguousarray(orders, dtype=np.int32),
+            p=g.fastgcn_p if kind == "fastgcn" else None)
+        feat, ld_feat, F, ld_x0 = None, 0, 0, 0
+        if store is not None:
+            F, ld_x0 = store.F, store.ld
+            if not store.zero_copy:
+                host = store.host
+                assert host.dtype == torch.float32 and host.stride(1) == 1
+                feat, ld_feat = host.data_ptr(), host.stride(0)
+                self._keep["feat"] = host
+        k = self._keep
+        ptr = lambda a: None if a is None else a.ctypes.data
+        if pinned is None:
+            pinned = torch.cuda.is_available()
+        L = _lib.sampler_lib()
+        self.handle = L.gnn_loader_create(
+            ptr(g.indptr), ptr(g.indices), ptr(g.data), g.num_nodes, ptr(k["lab_ptr"]), ptr(k["lab_idx"]),
+            ptr(k["lab_val"]), int(lab.shape[1]), ptr(k["dev_of"]), ptr(k["idx_on"]), rank, world_size,
+            ptr(k["devices"]), feat, ld_feat, F, ld_x0, ptr(k["samp"]), ptr(k["orders"]), nl, KINDS[kind],
+            ptr(k["p"]), int(bool(device_extract) and kind == "ladies"), 1, self.workers, int(bool(pinned)))
+        if not self.handle:
+            raise RuntimeError("gnn_loader_create failed: " + L.gnn_sampler_last_error().decode(errors="replace"))
+        self._pending = 0
+
+    def _submit(self, nodes) -> None:
+        from . import _lib
+
+        nodes = np.ascontiguousarray(nodes, dtype=np.int64)
+        seed = int(self.rng.randint(2**32 - 1))
+        _lib.check_sampler(_lib.sampler_lib().gnn_loader_submit(self.handle, seed, nodes.ctypes.data, nodes.size),
+                           "gnn_loader_submit")
+        self._pending += 1
+
+    def _next(self) -> LoadedBatch:
+        import ctypes
+
+        from . import _lib
+
+        h = ctypes.c_void_p()
+        self._pending -= 1
+        _lib.check_sampler(_lib.sampler_lib().gnn_loader_next(self.handle, ctypes.byref(h)), "gnn_loader_next")
+        nb = NativeBatch(h.value, self.store)
+        nb.graph = self.graph
+        return LoadedBatch(nb, nb.plan)
+
+    def epoch(self, iter_num: int) -> Iterator[LoadedBatch]:
+        return self._stream(smp.rank_batches(self.train, self.batch_size, self.rank, self.world, iter_num))
+
+    def forever(self, first_epoch: int = 1) -> Iterator[LoadedBatch]:
+        def chunks():
+            e = first_epoch
+            while True:
+                yield from smp.rank_batches(self.train, self.batch_size, self.rank, self.world, e)
+                e += 1
+        return self._stream(chunks())
+
+    def _stream(self, chunks) -> Iterator[LoadedBatch]:
+        it = iter(chunks)
+        done = False
+        while True:
+            while not done and self._pending < self.prefetch:
+                try:
+                    self._submit(next(it))
+                except StopIteration:
+                    done = True
+            if self._pending == 0:
+                return
+            yield self._next()
+
+    def close(self):
+        from . import _lib
+
+        if self.handle:
+            _lib.sampler_lib().gnn_loader_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -114,6 +114,7 @@ class StagePlan:
     peer_pos: List[np.ndarray]   # per peer rank: X0 rows it supplies
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
     pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos[, host_src])
+    blob: object = None          # a loader.NativeBatch: every array above lives in its blob, uploaded once
 
 
 def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devices=None) -> StagePlan:
@@ -174,22 +175,27 @@ class Stager:
         # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
             x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
-            idx = [t.to(dev, non_blocking=True) for t in plan.pinned]
-            own_pos, own_src, host_pos = idx[:3]
             nh = len(plan.host_pos)
             if self.timing is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-            if plan.host_rows is None:  # zero-copy: the GPU reads the rows from the mapped table
-                host_dev = idx[3]
-                cso.gather_rows_host(self.store.host, host_dev, x0, host_pos, n=nh)
+            if plan.blob is not None:  # native loader: ONE H2D of the whole batch blob, views of it
+                own_pos, own_src, host_pos, host_dev = plan.blob.stage_views(dev)
+                if self.store.zero_copy:  # host_dev = the host rows' node ids
+                    cso.gather_rows_host(self.store.host, host_dev, x0, host_pos, n=nh)
             else:
-                host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
+                idx = [t.to(dev, non_blocking=True) for t in plan.pinned]
+                own_pos, own_src, host_pos = idx[:3]
+                if plan.host_rows is None:  # zero-copy: the GPU reads the rows from the mapped table
+                    host_dev = idx[3]
+                    cso.gather_rows_host(self.store.host, host_dev, x0, host_pos, n=nh)
+                else:
+                    host_dev = plan.host_rows.to(dev, non_blocking=True)  # one contiguous H2D
             if self.timing is not None:
                 e1.record(st)
-                self.timing.append((e0, e1, nh * self.store.ld * 4))
+                self.timing.append((e0, e1, plan.blob.nbytes if plan.blob is not None else nh * self.store.ld * 4))
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
-            if nh and plan.host_rows is not None:
+            if nh and (plan.host_rows is not None or (plan.blob is not None and not self.store.zero_copy)):
                 cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
             extra = ()
             if self.exchange is not None:

@@ -103,6 +103,73 @@ int gnn_ladies_input_nodes(const gnn_ladies_result* r, int64_t* out);
 
 void gnn_ladies_free(gnn_ladies_result* r);
 
+/* ---------------------------------------------------------------------------------------
+ * Native batch producer (loader.cpp): prepare_data's thread pool (sampler.py:163-210) plus the
+ * host half of the feature staging (main.py:129-134) in C++ threads that never take the Python
+ * GIL. Each batch becomes ONE contiguous blob (pinned through the process's HIP runtime when it
+ * is loaded and `pinned` != 0) described by an int64 descriptor:
+ *   header  [GNN_BLOB_HEADER] slots GNN_H_*;
+ *   layer li (bottom-up) at GNN_BLOB_HEADER + li * GNN_BLOB_LAYER_SLOTS: scalars GNN_L_* and
+ *     sections (byte offset, element count) at the GNN_L_* section slots;
+ *   batch sections at GNN_BLOB_HEADER + num_layers * GNN_BLOB_LAYER_SLOTS + GNN_B_*, then per
+ *     peer j (world entries): peer_pos at + GNN_BLOB_BATCH_SLOTS + 4 j, peer_src at + 2.
+ * Sections are 256-byte aligned; absent sections have count 0. Element types: int32 for
+ * fullrowptr / rowptr / colidx / csc_colptr / csc_rows / rows / cols / rmap, fp32 for normfact,
+ * labels [batch x classes] and host_rows [n_host x ld_x0] (zero-padded rows of the feature
+ * table), int64 for sampled and every placement list. Layer semantics as gnn_ladies_sample_dev
+ * (device-extracted layers carry rows / cols / csc_colptr instead of the CSR pieces); rmap[K]
+ * (layers >= 1): rmap[sampled[i]] = i, -1 elsewhere. */
+#define GNN_BLOB_VERSION 1
+#define GNN_BLOB_MAX_LAYERS 16
+#define GNN_BLOB_HEADER 16
+#define GNN_BLOB_LAYER_SLOTS 32
+#define GNN_BLOB_BATCH_SLOTS 16
+enum {
+  GNN_H_VERSION = 0, GNN_H_LAYERS = 1, GNN_H_BYTES = 2, GNN_H_BATCH = 3, GNN_H_CLASSES = 4, GNN_H_INPUTS = 5,
+  GNN_H_WORLD = 6, GNN_H_LD_X0 = 7, GNN_H_SEED = 8, GNN_H_PINNED = 9
+};
+enum {
+  GNN_L_PRESENT = 0, GNN_L_ON_DEVICE = 1, GNN_L_M = 2, GNN_L_K = 3, GNN_L_NNZ = 4, GNN_L_SNUM = 5,
+  GNN_L_NSAMPLED = 6, GNN_L_HAS_RMAP = 7, GNN_L_FULLROWPTR = 8, GNN_L_ROWPTR = 10, GNN_L_COLIDX = 12,
+  GNN_L_NORMFACT = 14, GNN_L_CSC_COLPTR = 16, GNN_L_CSC_ROWS = 18, GNN_L_ROWS = 20, GNN_L_COLS = 22,
+  GNN_L_SAMPLED = 24, GNN_L_RMAP = 26
+};
+enum {
+  GNN_B_LABELS = 0, GNN_B_HOST_ROWS = 2, GNN_B_OWN_POS = 4, GNN_B_OWN_SRC = 6, GNN_B_HOST_POS = 8,
+  GNN_B_HOST_SRC = 10, GNN_B_INPUT_NODES = 12
+};
+enum { GNN_SAMPLER_LADIES = 0, GNN_SAMPLER_SUBGRAPH = 1, GNN_SAMPLER_FASTGCN = 2 };
+
+typedef struct gnn_loader gnn_loader;
+typedef struct gnn_batch gnn_batch;
+
+/* Borrowed arrays (the caller keeps them alive until gnn_loader_destroy): the graph as for the
+ * samplers; labels as CSR (int64 indptr, int32 indices, fp32 values, num_classes columns);
+ * the placement of this rank (device_id_of_nodes / idx_of_nodes_on_device, main.py:95-103),
+ * devices[world]; feat (NULL: no host-row gather, e.g. zero-copy staging) with row stride
+ * ld_feat, F features, host rows written ld_x0 wide. kind GNN_SAMPLER_*; fastgcn_p for FastGCN;
+ * device_extract as gnn_ladies_sample_dev; host-extracted layers >= csc_from also get their CSC.
+ * Returns NULL on bad arguments (message in gnn_sampler_last_error). */
+gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+                              const int64_t* label_indptr, const int32_t* label_indices, const float* label_values,
+                              int64_t num_classes, const int64_t* device_id_of_nodes,
+                              const int64_t* idx_of_nodes_on_device, int32_t rank, int32_t world,
+                              const int64_t* devices, const float* feat, int64_t ld_feat, int64_t F, int64_t ld_x0,
+                              const int64_t* samp_num, const int32_t* orders, int32_t num_layers, int32_t kind,
+                              const double* fastgcn_p, int32_t device_extract, int32_t csc_from, int32_t workers,
+                              int32_t pinned);
+/* Queue one batch (node ids copied); batches come out of gnn_loader_next in submission order. */
+int gnn_loader_submit(gnn_loader* ld, uint32_t seed, const int64_t* nodes, int64_t n);
+/* Block until the oldest submitted batch is ready. On a sampling error returns its status (the
+ * message in gnn_sampler_last_error) and *out = NULL. */
+int gnn_loader_next(gnn_loader* ld, gnn_batch** out);
+const int64_t* gnn_batch_desc(const gnn_batch* b, int64_t* n);
+void* gnn_batch_blob(const gnn_batch* b);
+/* Return the blob to its pool (call once the device copy that reads it has completed). */
+void gnn_batch_release(gnn_batch* b);
+/* Stops the threads (queued batches are dropped); batches already handed out stay valid. */
+void gnn_loader_destroy(gnn_loader* ld);
+
 /* Host half of the layer-0 feature staging (main.py:134, `feat_data[idx_cpu]`): copy rows
  * src[idx[i], 0:F] into dst row i (stride ld_dst, columns [F, ld_dst) zeroed) — typically a
  * pinned buffer that one hipMemcpyAsync then moves to the GPU. */

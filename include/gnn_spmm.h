@@ -170,6 +170,10 @@ int gnn_gather_rows_host_f32(const float* host_src, int64_t ld_src, const int64_
 int gnn_host_register(void* host, size_t bytes);
 int gnn_host_unregister(void* host);
 
+/* One stream-ordered host-to-device copy (hipMemcpyAsync): the upload of a native loader's
+ * batch blob (gnn_sampler.h) — every per-batch array of main.py:115-134 in one transfer. */
+int gnn_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

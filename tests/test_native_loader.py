@@ -1,0 +1,139 @@
+"""Native batch producer (libgnn_sampler.so gnn_loader_*, gnn_amd.loader.NativeLoader).
+
+CPU: for the same seed schedule the C++ workers produce exactly what the Python BatchLoader
+produces (whose sampler and placement are pinned to the reference by tests/golden): every layer
+array, the CSC of host-extracted layers, sampled nodes and residual row maps, dense labels, the
+placement split of the layer-0 inputs (own buffer / host / each peer), and the gathered host
+feature rows — for LADIES (host and device extraction), subgraph and FastGCN, at world sizes 1
+and 2. GPU: a NativeBatch uploads as one blob and its DeviceBatch / staged X0 equal the Python
+path's, operands bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gnn_amd import graphs, loader, placement, sampler, staging
+
+
+def _setup(world=1):
+    rng = np.random.default_rng(2)
+    A = graphs.chung_lu(12_000, 90_000, 1.3, rng)
+    lap = graphs.lap_matrix(A, "graphsage")
+    N = A.shape[0]
+
+    cls = rng.integers(0, 7, N)
+    import scipy.sparse as sp
+    labels = sp.csr_matrix((np.ones(N, np.int32), (np.arange(N), cls)), shape=(N, 7))
+    feats = torch.randn(N, 37, generator=torch.Generator().manual_seed(0))
+    train = np.arange(0, 8000)
+    pl = placement.create_buffer(lap, train, 1500, list(range(world)), 2, alpha=0)
+    return lap, labels, feats, train, pl
+
+
+def _loaders(kind, world, rank, dx, samp=400, bs=96):
+    lap, labels, feats, train, pl = _setup(world)
+    dev_of, idx_on = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], "cpu", rank)
+    kw = dict(rank=rank, world_size=world, store=store, workers=3, seed=9, kind=kind, device_extract=dx)
+    a = loader.BatchLoader(lap, labels, train, samp, bs, [1, 1, 1], dev_of, idx_on, **kw)
+    b = loader.NativeLoader(lap, labels, train, samp, bs, [1, 1, 1], dev_of, idx_on, **kw)
+    return a, b, store
+
+
+def _eq(x, y, what):
+    x = x.numpy() if isinstance(x, torch.Tensor) else np.asarray(x)
+    y = y.numpy() if isinstance(y, torch.Tensor) else np.asarray(y)
+    assert x.shape == y.shape and np.array_equal(x, y), what
+
+
+@pytest.mark.parametrize("kind,world,rank,dx", [("ladies", 1, 0, False), ("ladies", 1, 0, True),
+                                                ("ladies", 2, 1, True), ("subgraph", 1, 0, False),
+                                                ("fastgcn", 2, 0, False)])
+def test_native_loader_equals_python_loader(kind, world, rank, dx):
+    a, b, store = _loaders(kind, world, rank, dx)
+    try:
+        for pa, pb in zip(a.epoch(1), b.epoch(1)):
+            ha, hb = pa.host, pb.host
+            assert ha.seed == hb.seed
+            _eq(ha.input_nodes, hb.input_nodes, "input nodes")
+            _eq(ha.labels, hb.labels, "labels")
+            assert ha.nnz() == hb.nnz()
+            for li, (La, Lb) in enumerate(zip(ha.layers, hb.layers)):
+                assert (La is None) == (Lb is None)
+                if La is None:
+                    continue
+                assert La.shape == Lb.shape and La.on_device == Lb.on_device and La.nnz == Lb.nnz
+                for k in ("fullrowptr", "rowptr", "colidx", "normfact", "csc_colptr", "csc_rows", "rows", "cols"):
+                    va, vb = getattr(La, k), getattr(Lb, k)
+                    assert (va is None) == (vb is None), (li, k)
+                    if va is not None:
+                        _eq(va, vb, f"layer {li} {k}")
+            for li, (sa, sb) in enumerate(zip(ha.sampled_nodes, hb.sampled_nodes)):
+                _eq(np.asarray(sa, np.int64), sb, f"sampled {li}")
+            rmaps = ha.pin().extra["rmaps"]
+            for li in range(len(ha.layers)):
+                base = loader.BLOB_HEADER + li * loader.BLOB_LAYER_SLOTS
+                if rmaps[li] is not None:
+                    _eq(rmaps[li], hb._h(base + loader.L_RMAP, np.dtype(np.int32)), f"rmap {li}")
+            qa, qb = pa.plan, pb.plan
+            for k in ("own_pos", "own_src", "host_pos"):
+                _eq(getattr(qa, k), getattr(qb, k), k)
+            for j in range(world):
+                _eq(qa.peer_pos[j], qb.peer_pos[j], f"peer_pos {j}")
+                _eq(qa.peer_src[j], qb.peer_src[j], f"peer_src {j}")
+            bb = hb._bb
+            rows = hb._h(bb + loader.B_HOST_ROWS, np.dtype(np.float32)).reshape(-1, store.ld)
+            _eq(qa.host_rows, rows, "host rows")
+    finally:
+        a.close()
+        b.close()
+
+
+def test_native_loader_bad_batch_raises():
+    lap, labels, feats, train, pl = _setup()
+    b = loader.NativeLoader(lap, labels, train, 100, 16, [1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], workers=2)
+    try:
+        with pytest.raises(RuntimeError, match="out of range"):
+            b._submit(np.array([0, lap.shape[0] + 5]))
+    finally:
+        b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dx", [False, True])
+def test_native_batch_on_device(dev, dx):
+    lap, labels, feats, train, pl = _setup()
+    dev_of, idx_on = pl.device_id_of_nodes_group[0], pl.idx_of_nodes_on_device_group[0]
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    kw = dict(store=store, workers=2, seed=3, device_extract=dx)
+    a = loader.BatchLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
+    b = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
+    stager = staging.Stager(store)
+    try:
+        for n, (pa, pb) in enumerate(zip(a.epoch(1), b.epoch(1))):
+            sa = stager.issue(pa.plan, lambda: pa.host.to_device(dev, with_coo=False))
+            sb = stager.issue(pb.plan, lambda: pb.host.to_device(dev, with_coo=False))
+            xa, xb = sa.wait(), sb.wait()
+            torch.cuda.synchronize()
+            assert torch.equal(xa, xb)
+            ref = feats[torch.from_numpy(np.asarray(pa.host.input_nodes, np.int64))].to(dev)
+            assert torch.equal(xb, ref), "X0 rows = the feature table's rows"
+            da, db = sa.batch, sb.batch
+            assert torch.equal(da.labels, db.labels)
+            for x, y in zip(da.sampled_nodes, db.sampled_nodes):
+                assert torch.equal(x, y)
+                ra, rb = getattr(x, "_gnn_rmap", None), getattr(y, "_gnn_rmap", None)
+                assert (ra is None) == (rb is None) and (ra is None or torch.equal(ra, rb))
+            for li, (oa, ob) in enumerate(zip(sa.adjs, sb.adjs)):
+                for k in ("rowptr", "col", "val"):
+                    assert torch.equal(getattr(oa, k), getattr(ob, k)), (li, k)
+                if li >= 1:
+                    ta, tb = oa.transpose(), ob.transpose()
+                    for k in ("rowptr", "col", "val"):
+                        assert torch.equal(getattr(ta, k), getattr(tb, k)), (li, "t", k)
+            if n == 3:
+                break
+    finally:
+        a.close()
+        b.close()
