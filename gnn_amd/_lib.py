@@ -68,8 +68,9 @@ _SIGNATURES = {
     "gnn_head_bce_bwd_f32": (_INT, [_VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _VP, ctypes.c_float,
                                     ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _I64, _VP]),
     # include/gnn_extract.h
+    "gnn_ladies_extract_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int32]),
     "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP,
-                                      _VP, _VP, _VP, _VP, _VP, _VP]),
+                                      _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
     "gnn_gemm_f32_split3_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
@@ -85,9 +86,9 @@ _SAMPLER_SIGNATURES = {
     "gnn_sampler_last_error": (ctypes.c_char_p, []),
     "gnn_ladies_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                  ctypes.POINTER(_VP)]),
-    "gnn_ladies_sample_dev": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
+    "gnn_ladies_sample_dev": (_INT, [_VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                      ctypes.c_int32, ctypes.POINTER(_VP)]),
-    "gnn_ladies_layer_device": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP]),
+    "gnn_ladies_layer_device": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP]),
     "gnn_subgraph_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                    ctypes.POINTER(_VP)]),
     "gnn_fastgcn_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
@@ -100,7 +101,7 @@ _SAMPLER_SIGNATURES = {
     "gnn_ladies_free": (None, [_VP]),
     "gnn_mt19937_random_sample": (_INT, [ctypes.c_uint32, _I64, _VP]),
     "gnn_host_gather_rows_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _I64]),
-    "gnn_loader_create": (_VP, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32,
+    "gnn_loader_create": (_VP, [_VP, _VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32,
                                 _VP, _VP, _I64, _I64, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32, _VP,
                                 ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "gnn_loader_submit": (_INT, [_VP, ctypes.c_uint32, _VP, _I64]),

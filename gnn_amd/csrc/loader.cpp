@@ -135,6 +135,7 @@ struct gnn_loader {
   const int64_t* indptr;
   const int32_t* indices;
   const float* data;
+  const int64_t* indptr_t;
   int64_t N;
   const int64_t* lab_ptr;
   const int32_t* lab_idx;
@@ -220,6 +221,8 @@ void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batc
       secs.push_back({base + GNN_L_ROWS, L.M, 4});
       secs.push_back({base + GNN_L_COLS, L.K, 4});
       secs.push_back({base + GNN_L_CSC_COLPTR, L.K + 1, 4});
+      secs.push_back({base + GNN_L_FULLROWPTR, L.M + 1, 4});
+      secs.push_back({base + GNN_L_COLSEG, L.K + 1, 4});
     } else {
       secs.push_back({base + GNN_L_FULLROWPTR, L.M + 1, 4});
       secs.push_back({base + GNN_L_ROWPTR, L.M + 1, 4});
@@ -271,6 +274,8 @@ void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batc
       put(base + GNN_L_ROWS, L.rows.data(), L.M * 4);
       put(base + GNN_L_COLS, L.cols.data(), L.K * 4);
       put(base + GNN_L_CSC_COLPTR, L.colptr.data(), (L.K + 1) * 4);
+      put(base + GNN_L_FULLROWPTR, L.fullrowptr.data(), (L.M + 1) * 4);
+      put(base + GNN_L_COLSEG, L.colseg.data(), (L.K + 1) * 4);
     } else {
       put(base + GNN_L_FULLROWPTR, L.fullrowptr.data(), (L.M + 1) * 4);
       put(base + GNN_L_ROWPTR, L.rowptr.data(), (L.M + 1) * 4);
@@ -332,7 +337,7 @@ gnn_batch* gnn_loader::produce(const Job& job) {
     rc = gnn_subgraph_sample(indptr, indices, data, N, job.nodes.data(), (int64_t)job.nodes.size(), samp.data(),
                              orders.data(), nl, job.seed, &res);
   else
-    rc = gnn_ladies_sample_dev(indptr, indices, data, N, job.nodes.data(), (int64_t)job.nodes.size(), samp.data(),
+    rc = gnn_ladies_sample_dev(indptr, indices, data, indptr_t, N, job.nodes.data(), (int64_t)job.nodes.size(), samp.data(),
                                orders.data(), nl, job.seed, device_extract, &res);
   if (rc != 0) {
     b->rc = rc;
@@ -370,7 +375,8 @@ void gnn_loader::run() {
 
 extern "C" {
 
-gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, const float* data,
+                              const int64_t* indptr_t, int64_t num_nodes,
                               const int64_t* label_indptr, const int32_t* label_indices, const float* label_values,
                               int64_t num_classes, const int64_t* device_id_of_nodes,
                               const int64_t* idx_of_nodes_on_device, int32_t rank, int32_t world,
@@ -390,6 +396,7 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
     ld->indptr = indptr;
     ld->indices = indices;
     ld->data = data;
+    ld->indptr_t = indptr_t;
     ld->N = num_nodes;
     ld->lab_ptr = label_indptr;
     ld->lab_idx = label_indices;

@@ -237,18 +237,29 @@ class Work {
   // A layer left to the GPU extraction: its rows and columns as int32 node ids, and from the
   // column counts of U (structural: data == NULL) the exact nnz of U[:, after] and its CSC
   // column pointer — colptr[j + 1] - colptr[j] = count of U's column after[j].
-  void device_layer(const std::vector<int64_t>& prev, const std::vector<int64_t>& after, Layer& L) const {
+  // colseg: the offsets of lapᵀ's rows of `after` concatenated (the transposed extraction's
+  // segments), from indptr_t (lapᵀ's row pointer; the graph's own when NULL = symmetric).
+  // Returns false if they reach 2^31 entries.
+  bool device_layer(const std::vector<int64_t>& prev, const std::vector<int64_t>& after, const int64_t* indptr_t,
+                    Layer& L) const {
     L.on_device = true;
     L.rows.assign(prev.begin(), prev.end());
     L.cols.assign(after.begin(), after.end());
     L.colptr.resize(after.size() + 1);
-    int64_t acc = 0;
+    L.colseg.resize(after.size() + 1);
+    const int64_t* pt = indptr_t ? indptr_t : g_.indptr;
+    int64_t acc = 0, seg = 0;
     L.colptr[0] = 0;
+    L.colseg[0] = 0;
     for (size_t j = 0; j < after.size(); ++j) {
       acc += cnt[(size_t)after[j]];
       L.colptr[j + 1] = (int32_t)acc;
+      seg += pt[after[j] + 1] - pt[after[j]];
+      if (seg >= ((int64_t)1 << 31)) return false;
+      L.colseg[j + 1] = (int32_t)seg;
     }
     L.nnz = acc;
+    return true;
   }
 
   void set_columns(const std::vector<int64_t>& cols) {
@@ -374,11 +385,12 @@ int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out) {
 int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out) {
-  return gnn_ladies_sample_dev(indptr, indices, data, num_nodes, batch_nodes, batch_size, samp_num, orders,
+  return gnn_ladies_sample_dev(indptr, indices, data, nullptr, num_nodes, batch_nodes, batch_size, samp_num, orders,
                                num_layers, seed, 0, out);
 }
 
-int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, const int64_t* indptr_t,
+                          int64_t num_nodes,
                           const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                           const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
                           gnn_ladies_result** out) {
@@ -422,8 +434,8 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
       w.make_after(prev, after, !dev);
       if (dev) {
-        w.device_layer(prev, after, L);
-        if (L.nnz >= ((int64_t)1 << 31)) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
+        if (!w.device_layer(prev, after, indptr_t, L) || L.nnz >= ((int64_t)1 << 31))
+          return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
       } else {
         w.extract(prev, unnz, L);
       }
@@ -585,13 +597,15 @@ int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fu
 }
 
 int gnn_ladies_layer_device(const gnn_ladies_result* r, int32_t layer, int32_t* rows, int32_t* cols,
-                            int32_t* colptr) {
+                            int32_t* colptr, int32_t* rowseg, int32_t* colseg) {
   if (!r || layer < 0 || (size_t)layer >= r->layers.size()) return fail("gnn_ladies_layer_device: bad args");
   const Layer& L = r->layers[(size_t)layer];
   if (!L.present || !L.on_device) return 1;
   if (rows && !L.rows.empty()) std::memcpy(rows, L.rows.data(), L.rows.size() * 4);
   if (cols && !L.cols.empty()) std::memcpy(cols, L.cols.data(), L.cols.size() * 4);
   if (colptr) std::memcpy(colptr, L.colptr.data(), L.colptr.size() * 4);
+  if (rowseg) std::memcpy(rowseg, L.fullrowptr.data(), L.fullrowptr.size() * 4);
+  if (colseg) std::memcpy(colseg, L.colseg.data(), L.colseg.size() * 4);
   return 0;
 }
 

@@ -18,6 +18,7 @@ struct Layer {
   std::vector<float> normfact;
   std::vector<int64_t> sampled;
   std::vector<int32_t> rows, cols, colptr;  // on_device: U's rows, after_nodes, CSC column pointer
+  std::vector<int32_t> colseg;              // on_device: offsets of lapᵀ's rows of after_nodes (K+1)
 };
 
 // Stable counting sort of a host-extracted layer's entries by column: the CSC (colptr[K+1],

@@ -348,14 +348,16 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
 
 
 def extract_operand(graph, rows: torch.Tensor, cols: torch.Tensor, normfact: torch.Tensor, nnz: int,
+                    rowseg: torch.Tensor, colseg: Optional[torch.Tensor] = None,
                     colptr: Optional[torch.Tensor] = None) -> CsrOperand:
     """adj = lap[rows, :][:, cols] with create_coo_tensor's values, built on the GPU from the
     graph resident there (gnn_ladies_extract_f32; ``graph`` a sampler.DeviceGraph): the
     operand of a LADIES layer whose draw ran on the host (sampler.py:114-139). ``nnz`` is the
-    host-known entry count (the column counts of U over cols). With ``colptr`` (the CSC column
+    host-known entry count (the column counts of U over cols); ``rowseg`` U's row pointer (M+1).
+    With ``colseg`` (offsets of lapᵀ's rows of cols, K+1) and ``colptr`` (the CSC column
     pointer, K+1; rows must be unique and ascending) the transpose is built too and cached on
     the operand — the canonical Aᵀ (A.t().coalesce())."""
-    for name, t in (("rows", rows), ("cols", cols)):
+    for name, t in (("rows", rows), ("cols", cols), ("rowseg", rowseg)):
         _require(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), f"{name} must be contiguous int32 CUDA")
     _require(normfact.is_cuda and normfact.dtype == torch.float32 and normfact.numel() == cols.numel(),
              "normfact must be float32 CUDA with one entry per column")
@@ -365,18 +367,23 @@ def extract_operand(graph, rows: torch.Tensor, cols: torch.Tensor, normfact: tor
         rowptr = torch.empty(M + 1, dtype=torch.int32, device=dev)
         col = torch.empty(nnz, dtype=torch.int32, device=dev)
         val = torch.empty(nnz, dtype=torch.float32, device=dev)
-        rowcnt = torch.empty(max(M, 1), dtype=torch.int32, device=dev)
         rows_t = val_t = None
+        _require(rowseg.numel() == M + 1, "rowseg must have M + 1 entries")
+        _require((colptr is None) == (colseg is None), "colptr and colseg come together")
         if colptr is not None:
-            _require(colptr.is_cuda and colptr.dtype == torch.int32 and colptr.numel() == K + 1,
-                     "colptr must be int32 CUDA with K + 1 entries")
+            for name, t in (("colptr", colptr), ("colseg", colseg)):
+                _require(t.is_cuda and t.dtype == torch.int32 and t.numel() == K + 1,
+                         f"{name} must be int32 CUDA with K + 1 entries")
             rows_t = torch.empty(nnz, dtype=torch.int32, device=dev)
             val_t = torch.empty(nnz, dtype=torch.float32, device=dev)
+        L = _lib.lib()
+        wsb = L.gnn_ladies_extract_workspace_bytes(graph.num_nodes, M, K, int(colptr is not None))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         st = _stream(dev)
-        _lib.check(_lib.lib().gnn_ladies_extract_f32(
+        _lib.check(L.gnn_ladies_extract_f32(
             _ptr(graph.indptr), _ptr(graph.indices), graph.num_nodes, _ptr(graph.indptr_t), _ptr(graph.indices_t),
-            _ptr(rows), M, _ptr(cols), K, _ptr(normfact), nnz, _ptr(colptr), _ptr(graph.node_map(st)),
-            _ptr(rowptr), _ptr(col), _ptr(val), _ptr(rowcnt), _ptr(rows_t), _ptr(val_t), _ptr(graph.err), st),
+            _ptr(rows), M, _ptr(cols), K, _ptr(normfact), nnz, _ptr(rowseg), _ptr(colseg), _ptr(colptr),
+            _ptr(rowptr), _ptr(col), _ptr(val), _ptr(rows_t), _ptr(val_t), ws.data_ptr(), wsb, _ptr(graph.err), st),
             "gnn_ladies_extract_f32")
     op = CsrOperand(rowptr, col, val, (M, K))
     if colptr is not None:

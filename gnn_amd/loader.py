@@ -152,8 +152,8 @@ class BatchLoader:
 BLOB_VERSION, BLOB_HEADER, BLOB_LAYER_SLOTS, BLOB_BATCH_SLOTS = 1, 16, 32, 16
 H_VERSION, H_LAYERS, H_BYTES, H_BATCH, H_CLASSES, H_INPUTS, H_WORLD, H_LD_X0, H_SEED, H_PINNED = range(10)
 (L_PRESENT, L_ON_DEVICE, L_M, L_K, L_NNZ, L_SNUM, L_NSAMPLED, L_HAS_RMAP) = range(8)
-L_FULLROWPTR, L_ROWPTR, L_COLIDX, L_NORMFACT, L_CSC_COLPTR, L_CSC_ROWS, L_ROWS, L_COLS, L_SAMPLED, L_RMAP = \
-    range(8, 28, 2)
+L_FULLROWPTR, L_ROWPTR, L_COLIDX, L_NORMFACT, L_CSC_COLPTR, L_CSC_ROWS, L_ROWS, L_COLS, L_SAMPLED, L_RMAP, \
+    L_COLSEG = range(8, 30, 2)
 B_LABELS, B_HOST_ROWS, B_OWN_POS, B_OWN_SRC, B_HOST_POS, B_HOST_SRC, B_INPUT_NODES = range(0, 14, 2)
 KINDS = {"ladies": 0, "subgraph": 1, "fastgcn": 2}
 _I32, _I64, _F32 = np.dtype(np.int32), np.dtype(np.int64), np.dtype(np.float32)
@@ -223,10 +223,11 @@ class NativeBatch:
                     continue
                 shape = (int(self.desc[b + L_M]), int(self.desc[b + L_K]))
                 if self.desc[b + L_ON_DEVICE]:
-                    out.append(HostLayer(fullrowptr=None, rowptr=None, colidx=None, normfact=self._h(b + L_NORMFACT, _F32),
-                                         shape=shape, csc_colptr=self._h(b + L_CSC_COLPTR, _I32),
+                    out.append(HostLayer(fullrowptr=self._h(b + L_FULLROWPTR, _I32), rowptr=None, colidx=None,
+                                         normfact=self._h(b + L_NORMFACT, _F32), shape=shape,
+                                         csc_colptr=self._h(b + L_CSC_COLPTR, _I32),
                                          rows=self._h(b + L_ROWS, _I32), cols=self._h(b + L_COLS, _I32),
-                                         dev_nnz=int(self.desc[b + L_NNZ])))
+                                         dev_nnz=int(self.desc[b + L_NNZ]), colseg=self._h(b + L_COLSEG, _I32)))
                 else:
                     has_t = self._count(b + L_CSC_COLPTR) > 0
                     out.append(HostLayer(fullrowptr=self._h(b + L_FULLROWPTR, _I32), rowptr=self._h(b + L_ROWPTR, _I32),
@@ -294,13 +295,15 @@ class NativeBatch:
                 continue
             shape = (int(self.desc[b + L_M]), int(self.desc[b + L_K]))
             if self.desc[b + L_ON_DEVICE]:
-                raw.append((None, None, None, self._d(b + L_NORMFACT, _F32), shape, self._d(b + L_CSC_COLPTR, _I32), None,
-                            self._d(b + L_ROWS, _I32), self._d(b + L_COLS, _I32), int(self.desc[b + L_NNZ])))
+                raw.append((self._d(b + L_FULLROWPTR, _I32), None, None, self._d(b + L_NORMFACT, _F32), shape,
+                            self._d(b + L_CSC_COLPTR, _I32), None, self._d(b + L_ROWS, _I32),
+                            self._d(b + L_COLS, _I32), int(self.desc[b + L_NNZ]), self._d(b + L_COLSEG, _I32)))
             else:
                 has_t = self._count(b + L_CSC_COLPTR) > 0
                 raw.append((self._d(b + L_FULLROWPTR, _I32), self._d(b + L_ROWPTR, _I32), self._d(b + L_COLIDX, _I32),
                             self._d(b + L_NORMFACT, _F32), shape, self._d(b + L_CSC_COLPTR, _I32) if has_t else None,
-                            self._d(b + L_CSC_ROWS, _I32) if has_t else None, None, None, int(self.desc[b + L_NNZ])))
+                            self._d(b + L_CSC_ROWS, _I32) if has_t else None, None, None, int(self.desc[b + L_NNZ]),
+                            None))
         sn = []
         for li in range(self.num_layers):
             b = self._lb(li)
@@ -371,11 +374,13 @@ class NativeLoader:
         if pinned is None:
             pinned = torch.cuda.is_available()
         L = _lib.sampler_lib()
+        dx = int(bool(device_extract) and kind == "ladies" and g.data is None)
+        ipt = g.transpose_structure[1] if dx else None
         self.handle = L.gnn_loader_create(
-            ptr(g.indptr), ptr(g.indices), ptr(g.data), g.num_nodes, ptr(k["lab_ptr"]), ptr(k["lab_idx"]),
+            ptr(g.indptr), ptr(g.indices), ptr(g.data), ptr(ipt), g.num_nodes, ptr(k["lab_ptr"]), ptr(k["lab_idx"]),
             ptr(k["lab_val"]), int(lab.shape[1]), ptr(k["dev_of"]), ptr(k["idx_on"]), rank, world_size,
             ptr(k["devices"]), feat, ld_feat, F, ld_x0, ptr(k["samp"]), ptr(k["orders"]), nl, KINDS[kind],
-            ptr(k["p"]), int(bool(device_extract) and kind == "ladies"), 1, self.workers, int(bool(pinned)))
+            ptr(k["p"]), dx, 1, self.workers, int(bool(pinned)))
         if not self.handle:
             raise RuntimeError("gnn_loader_create failed: " + L.gnn_sampler_last_error().decode(errors="replace"))
         self._pending = 0

@@ -33,12 +33,14 @@ class HostLayer:
     shape: tuple            # (M, K)
     csc_colptr: Optional[np.ndarray] = None  # int32 [K+1]: CSC of the sub-graph (= CSR of its
     csc_rows: Optional[np.ndarray] = None    # transpose, rows ascending per column), if made
-    # A layer left to the GPU extraction (gnn_ladies_extract_f32): fullrowptr / rowptr / colidx
-    # are None; rows = U's rows (node ids, ascending), cols = after_nodes, csc_colptr from the
-    # column counts, dev_nnz = its exact nnz.
+    # A layer left to the GPU extraction (gnn_ladies_extract_f32): rowptr / colidx are None;
+    # rows = U's rows (node ids, ascending), cols = after_nodes, csc_colptr from the column
+    # counts, fullrowptr = U's row pointer (the forward segments), colseg = the offsets of lapᵀ's
+    # rows of cols (the transposed segments), dev_nnz = its exact nnz.
     rows: Optional[np.ndarray] = None
     cols: Optional[np.ndarray] = None
     dev_nnz: int = -1
+    colseg: Optional[np.ndarray] = None
 
     @property
     def on_device(self) -> bool:
@@ -79,7 +81,7 @@ class HostBatch:
             p = lambda x: None if x is None else (t(x).pin_memory() if pin else t(x))
             layers = [None if L is None else
                       (p(L.fullrowptr), p(L.rowptr), p(L.colidx), p(L.normfact), p(L.csc_colptr), p(L.csc_rows),
-                       p(L.rows), p(L.cols))
+                       p(L.rows), p(L.cols), p(L.colseg))
                       for L in self.layers]
             sampled = [p(t(s, np.int64)) for s in self.sampled_nodes]
             self.extra["pinned"] = (layers, sampled, p(t(self.labels)))
@@ -127,7 +129,7 @@ class HostBatch:
         layers, sampled, labels = self.pin().extra["pinned"]
         d = lambda x: None if x is None else x.to(dev, non_blocking=True)
         raw = [None if P is None else (d(P[0]), d(P[1]), d(P[2]), d(P[3]), L.shape, d(P[4]), d(P[5]), d(P[6]),
-                                       d(P[7]), L.nnz)
+                                       d(P[7]), L.nnz, d(P[8]))
                for P, L in zip(layers, self.layers)]
         sn = [d(s) for s in sampled]
         for x, r in zip(sn, self.extra["rmaps"]):
@@ -145,7 +147,7 @@ class HostBatch:
 class DeviceBatch:
     host: HostBatch
     raw: list            # per layer: device (fullrowptr, rowptr, colidx, normfact, shape, csc_colptr|None,
-                         # csc_rows|None, rows|None, cols|None, nnz) or None
+                         # csc_rows|None, rows|None, cols|None, nnz, colseg|None) or None
     adjs: Optional[list]
     sampled_nodes: list
     labels: torch.Tensor
@@ -154,7 +156,7 @@ class DeviceBatch:
     def tensors(self) -> list:
         """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
         maps), labels and the built operands (record_stream across streams)."""
-        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6], r[7], r[8])
+        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6], r[7], r[8], r[10])
               if t is not None]
         for x in self.sampled_nodes:
             ts.append(x)
@@ -176,10 +178,11 @@ class DeviceBatch:
             if r is None:
                 adjs.append(None)
                 continue
-            fr, rp, ci, nf, shape, cp, cr, rows, cols, nnz = r
+            fr, rp, ci, nf, shape, cp, cr, rows, cols, nnz, cs = r
             if ci is None:  # left to the GPU extraction (rows / cols / column counts from the draw)
                 _require_graph(self.graph)
-                op = cso.extract_operand(self.graph, rows, cols, nf, nnz, cp if li >= csc_from else None)
+                tr = li >= csc_from
+                op = cso.extract_operand(self.graph, rows, cols, nf, nnz, fr, cs if tr else None, cp if tr else None)
                 coo = op.to_torch_coo()._indices() if with_coo else None
             else:
                 op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo,
@@ -204,8 +207,7 @@ def _require_graph(graph) -> None:
 class DeviceGraph:
     """A NativeGraph's structure resident in device memory for gnn_ladies_extract_f32: canonical
     CSR of lap (int64 indptr, int32 indices) and of lapᵀ (the same arrays when the structure is
-    symmetric), one node map per stream (int32[N], -1 between calls) and an error flag the
-    extraction raises if a device count disagrees with the host's."""
+    symmetric), and an error flag the extraction raises if a device count disagrees with the host's."""
 
     def __init__(self, graph: "NativeGraph", device):
         dev = torch.device(device)
@@ -213,25 +215,13 @@ class DeviceGraph:
         self.num_nodes = graph.num_nodes
         self.indptr = torch.from_numpy(graph.indptr).to(dev)
         self.indices = torch.from_numpy(graph.indices).to(dev)
-        lt = graph.lap.T.tocsr()
-        lt.sum_duplicates()
-        lt.sort_indices()
-        self.symmetric = bool(np.array_equal(lt.indptr, graph.indptr) and np.array_equal(lt.indices, graph.indices))
+        self.symmetric, ipt, ixt = graph.transpose_structure
         if self.symmetric:
             self.indptr_t, self.indices_t = self.indptr, self.indices
         else:
-            self.indptr_t = torch.from_numpy(np.ascontiguousarray(lt.indptr, dtype=np.int64)).to(dev)
-            self.indices_t = torch.from_numpy(np.ascontiguousarray(lt.indices, dtype=np.int32)).to(dev)
+            self.indptr_t = torch.from_numpy(ipt).to(dev)
+            self.indices_t = torch.from_numpy(ixt).to(dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._maps = {}
-
-    def node_map(self, stream: int) -> torch.Tensor:
-        """The node map of `stream` (created on first use, on the current stream = `stream`)."""
-        m = self._maps.get(stream)
-        if m is None:
-            m = torch.full((self.num_nodes,), -1, dtype=torch.int32, device=self.device)
-            self._maps[stream] = m
-        return m
 
     def check(self) -> None:
         """Raise if any extraction so far saw a count that disagrees with the host's (syncs)."""
@@ -281,6 +271,20 @@ class NativeGraph:
         self.lap = lap
         self._fastgcn_p = None
         self._device_graphs = {}
+        self._tstruct = None
+
+    @property
+    def transpose_structure(self):
+        """(symmetric, indptr_t, indices_t): lapᵀ's canonical structure, computed once; the two
+        arrays are None when it equals lap's (then lap's serve for both)."""
+        if self._tstruct is None:
+            lt = self.lap.T.tocsr()
+            lt.sum_duplicates()
+            lt.sort_indices()
+            sym = bool(np.array_equal(lt.indptr, self.indptr) and np.array_equal(lt.indices, self.indices))
+            self._tstruct = (sym, None if sym else np.ascontiguousarray(lt.indptr, dtype=np.int64),
+                             None if sym else np.ascontiguousarray(lt.indices, dtype=np.int32))
+        return self._tstruct
 
     @property
     def fastgcn_p(self) -> np.ndarray:
@@ -326,7 +330,9 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
     if kind == "fastgcn":
         rc = L.gnn_fastgcn_sample(*g3, ptr(graph.fastgcn_p), *rest)
     elif kind == "ladies" and device_extract:
-        rc = L.gnn_ladies_sample_dev(*g3, *rest[:-1], 1, rest[-1])
+        ipt = graph.transpose_structure[1]
+        rc = L.gnn_ladies_sample_dev(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), ptr(ipt), graph.num_nodes,
+                                     *rest[:-1], 1, rest[-1])
     else:
         rc = (L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample)(*g3, *rest)
     _lib.check_sampler(rc, f"gnn_{kind}_sample")
@@ -353,23 +359,24 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
                 continue
             M, K, nnz, ns = dims[0], dims[1], dims[2], dims[3]
             (tnf, nf), (tsa, sa) = buf(K, torch.float32), buf(ns, torch.int64)
-            if device_extract and L.gnn_ladies_layer_device(h, li, None, None, None) == 0:
+            if device_extract and L.gnn_ladies_layer_device(h, li, None, None, None, None, None) == 0:
                 (trw, rw), (tcl, cl), (tcp, cp) = buf(M, torch.int32), buf(K, torch.int32), buf(K + 1, torch.int32)
-                _lib.check_sampler(L.gnn_ladies_layer_device(h, li, ptr(rw), ptr(cl), ptr(cp)) & ~1,
+                (tfr, fr), (tcs, cs) = buf(M + 1, torch.int32), buf(K + 1, torch.int32)
+                _lib.check_sampler(L.gnn_ladies_layer_device(h, li, ptr(rw), ptr(cl), ptr(cp), ptr(fr), ptr(cs)) & ~1,
                                    "gnn_ladies_layer_device")
                 _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, None, None, None, ptr(nf), ptr(sa)),
                                    "gnn_ladies_layer_copy")
-                pinned_layers.append((None, None, None, tnf, tcp, None, trw, tcl))
+                pinned_layers.append((tfr, None, None, tnf, tcp, None, trw, tcl, tcs))
                 pinned_sampled.append(tsa)
-                layers.append(HostLayer(fullrowptr=None, rowptr=None, colidx=None, normfact=nf, shape=(int(M), int(K)),
-                                        csc_colptr=cp, rows=rw, cols=cl, dev_nnz=int(nnz)))
+                layers.append(HostLayer(fullrowptr=fr, rowptr=None, colidx=None, normfact=nf, shape=(int(M), int(K)),
+                                        csc_colptr=cp, rows=rw, cols=cl, dev_nnz=int(nnz), colseg=cs))
                 sampled.append(sa)
                 continue
             (tfr, fr), (trp, rp), (tci, ci) = buf(M + 1, torch.int32), buf(M + 1, torch.int32), buf(nnz, torch.int32)
             tcp = tcr = cp = cr = None
             if li >= csc_from:  # layers whose input needs a gradient: the backward's operand
                 (tcp, cp), (tcr, cr) = buf(K + 1, torch.int32), buf(nnz, torch.int32)
-            pinned_layers.append((tfr, trp, tci, tnf, tcp, tcr, None, None))
+            pinned_layers.append((tfr, trp, tci, tnf, tcp, tcr, None, None, None))
             pinned_sampled.append(tsa)
             _lib.check_sampler(L.gnn_ladies_layer_copy(h, li, ptr(fr), ptr(rp), ptr(ci), ptr(nf), ptr(sa)),
                                "gnn_ladies_layer_copy")

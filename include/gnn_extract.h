@@ -32,22 +32,28 @@ extern "C" {
  * indptr / indices when the structure is symmetric). deg(v) = indptr[v+1] - indptr[v].
  * rows  int32[M]: U's rows (node ids) in order; cols int32[K]: after_nodes, strictly ascending;
  * normfact fp32[K]; nnz = number of entries of U[:, cols] (the sum of U's column counts over cols).
- * node_map int32[num_nodes]: workspace, every entry -1 on entry, restored to -1 (stream order);
- * one map per stream. rowcnt int32[M]: workspace.
+ * rowseg int32[M+1] = U's row pointer (exclusive scan of deg(rows[i])); colseg int32[K+1] = the
+ * exclusive scan of lapᵀ's row lengths of cols (transpose only) — both host-known (the draw).
+ * workspace: gnn_ladies_extract_workspace_bytes(num_nodes, M, K, transpose) bytes (no state is
+ * kept between calls: concurrent calls on different streams need different workspaces).
  * Outputs: rowptr int32[M+1], col int32[nnz] (positions into cols, ascending per row),
  * val fp32[nnz] = (float)((1.0 / deg(rows[i])) * (double)normfact[col]) — identical to
- * gnn_build_operand_f32 on the host-extracted pieces with fullrowptr = the rows' degrees.
- * Transpose (colptr_t != NULL; rows must then be unique and ascending): colptr_t int32[K+1] is
- * the CSC column pointer (host-known: the column counts), rows_t int32[nnz] / val_t fp32[nnz]
- * receive the canonical CSR of adj^T (rows ascending in each column) — what
+ * gnn_build_operand_f32 on the host-extracted pieces with fullrowptr = rowseg.
+ * Transpose (colptr_t != NULL; rows must then be unique and ascending): rows_t int32[nnz] /
+ * val_t fp32[nnz] receive the canonical CSR of adj^T (rows ascending in each column) whose row
+ * pointer is colptr_t, the host's CSC column pointer (its column counts; not read here) — what
  * gnn_csr_transpose / A.t().coalesce() would produce.
- * err_flag (device int32, optional): OR-ed with 1 if the device row counts do not add up to nnz,
- * 2 if a column's count differs from colptr_t (writes stay clamped inside their segments). */
+ * Work is balanced over entries, not rows (power-law rows): a fixed number of waves per
+ * direction each take a contiguous range of the concatenated graph rows; membership of a node
+ * in cols / rows is a bitmap + per-word rank table, staged in LDS when it fits.
+ * err_flag (device int32, optional): OR-ed with 1 / 2 if the kept entries of A / A^T do not add up
+ * to nnz (the writes stay inside the outputs). */
+size_t gnn_ladies_extract_workspace_bytes(int64_t num_nodes, int64_t M, int64_t K, int32_t transpose);
 int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, int64_t num_nodes, const int64_t* indptr_t,
                            const int32_t* indices_t, const int32_t* rows, int64_t M, const int32_t* cols, int64_t K,
-                           const float* normfact, int64_t nnz, const int32_t* colptr_t, int32_t* node_map,
-                           int32_t* rowptr, int32_t* col, float* val, int32_t* rowcnt, int32_t* rows_t, float* val_t,
-                           int32_t* err_flag, void* stream);
+                           const float* normfact, int64_t nnz, const int32_t* rowseg, const int32_t* colseg,
+                           const int32_t* colptr_t, int32_t* rowptr, int32_t* col, float* val, int32_t* rows_t,
+                           float* val_t, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream);
 
 #ifdef __cplusplus
 }

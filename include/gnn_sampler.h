@@ -47,8 +47,11 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
  * the layer's rows, columns, exact nnz and CSC column pointer for gnn_ladies_extract_f32
  * (include/gnn_extract.h), which builds adj = U[:, after] and its transpose on the GPU from the
  * graph resident there. Requires data == NULL (no stored zeros: the column counts are then the
- * structural counts the extraction keeps). The top layer (rows = the batch) is host-extracted. */
-int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+ * structural counts the extraction keeps). The top layer (rows = the batch) is host-extracted.
+ * indptr_t: lapᵀ's row pointer (NULL: the structure is symmetric, lapᵀ's = indptr) — for the
+ * offsets of the transposed extraction's segments. */
+int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const float* data, const int64_t* indptr_t,
+                          int64_t num_nodes,
                           const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                           const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
                           gnn_ladies_result** out);
@@ -84,12 +87,14 @@ int gnn_ladies_layer_copy(const gnn_ladies_result* r, int32_t layer, int32_t* fu
                           int32_t* colidx, float* normfact, int64_t* sampled);
 
 /* A layer left to the device extraction: rows int32[M] (U's rows, node ids), cols int32[K]
- * (after_nodes, ascending), colptr int32[K+1] (CSC column pointer of adj; colptr[K] = nnz).
+ * (after_nodes, ascending), colptr int32[K+1] (CSC column pointer of adj; colptr[K] = nnz),
+ * rowseg int32[M+1] (U's row pointer = the offsets of lap's rows of `rows` concatenated),
+ * colseg int32[K+1] (the offsets of lapᵀ's rows of `cols` concatenated).
  * Returns 0 and copies (NULL pointers skip) for such a layer, 1 for a host-extracted or absent
- * layer (nothing copied). fullrowptr / rowptr / colidx of gnn_ladies_layer_copy are not made for
- * it; normfact and sampled are. */
+ * layer (nothing copied). rowptr / colidx of gnn_ladies_layer_copy are not made for it;
+ * fullrowptr (= rowseg), normfact and sampled are. */
 int gnn_ladies_layer_device(const gnn_ladies_result* r, int32_t layer, int32_t* rows, int32_t* cols,
-                            int32_t* colptr);
+                            int32_t* colptr, int32_t* rowseg, int32_t* colseg);
 
 /* CSC structure of layer `layer`'s sub-graph (= CSR of its transpose, canonical: rows
  * ascending inside each column): colptr int32[K+1], rows int32[nnz]. Lets the training
@@ -117,7 +122,8 @@ void gnn_ladies_free(gnn_ladies_result* r);
  * fullrowptr / rowptr / colidx / csc_colptr / csc_rows / rows / cols / rmap, fp32 for normfact,
  * labels [batch x classes] and host_rows [n_host x ld_x0] (zero-padded rows of the feature
  * table), int64 for sampled and every placement list. Layer semantics as gnn_ladies_sample_dev
- * (device-extracted layers carry rows / cols / csc_colptr instead of the CSR pieces); rmap[K]
+ * (device-extracted layers carry rows / cols / csc_colptr / fullrowptr (= rowseg) / colseg
+ * instead of the CSR pieces, int32); rmap[K]
  * (layers >= 1): rmap[sampled[i]] = i, -1 elsewhere. */
 #define GNN_BLOB_VERSION 1
 #define GNN_BLOB_MAX_LAYERS 16
@@ -132,7 +138,7 @@ enum {
   GNN_L_PRESENT = 0, GNN_L_ON_DEVICE = 1, GNN_L_M = 2, GNN_L_K = 3, GNN_L_NNZ = 4, GNN_L_SNUM = 5,
   GNN_L_NSAMPLED = 6, GNN_L_HAS_RMAP = 7, GNN_L_FULLROWPTR = 8, GNN_L_ROWPTR = 10, GNN_L_COLIDX = 12,
   GNN_L_NORMFACT = 14, GNN_L_CSC_COLPTR = 16, GNN_L_CSC_ROWS = 18, GNN_L_ROWS = 20, GNN_L_COLS = 22,
-  GNN_L_SAMPLED = 24, GNN_L_RMAP = 26
+  GNN_L_SAMPLED = 24, GNN_L_RMAP = 26, GNN_L_COLSEG = 28
 };
 enum {
   GNN_B_LABELS = 0, GNN_B_HOST_ROWS = 2, GNN_B_OWN_POS = 4, GNN_B_OWN_SRC = 6, GNN_B_HOST_POS = 8,
@@ -150,7 +156,8 @@ typedef struct gnn_batch gnn_batch;
  * ld_feat, F features, host rows written ld_x0 wide. kind GNN_SAMPLER_*; fastgcn_p for FastGCN;
  * device_extract as gnn_ladies_sample_dev; host-extracted layers >= csc_from also get their CSC.
  * Returns NULL on bad arguments (message in gnn_sampler_last_error). */
-gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
+gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, const float* data,
+                              const int64_t* indptr_t, int64_t num_nodes,
                               const int64_t* label_indptr, const int32_t* label_indices, const float* label_values,
                               int64_t num_classes, const int64_t* device_id_of_nodes,
                               const int64_t* idx_of_nodes_on_device, int32_t rank, int32_t world,

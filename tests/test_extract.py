@@ -82,6 +82,10 @@ def test_device_draw_equals_host_draw(case):
             continue
         assert D.on_device and D.colidx is None
         assert D.nnz == L.colidx.size
+        assert np.array_equal(D.fullrowptr, L.fullrowptr), "rowseg = U's row pointer"
+        lt = sp.csr_matrix(_graph(case[0]).T)
+        degt = np.diff(lt.indptr)[D.cols]
+        assert np.array_equal(D.colseg, np.concatenate([[0], np.cumsum(degt)]).astype(np.int32))
         K = L.shape[1]
         colptr = np.concatenate([[0], np.cumsum(np.bincount(L.colidx, minlength=K))]).astype(np.int32)
         assert np.array_equal(D.csc_colptr, colptr)
@@ -131,8 +135,6 @@ def test_gpu_extraction_bitexact(dev, case):
                 assert torch.equal(getattr(at, k), getattr(bt2, k)), f"layer {li} gpu transpose {k}"
     dd.graph.check()
     assert dd.graph.symmetric == (case[0] == "symmetric")
-    m = dd.graph.node_map(torch.cuda.current_stream(dev).cuda_stream)
-    assert bool((m == -1).all()), "node map restored"
 
 
 @pytest.mark.gpu
@@ -142,18 +144,27 @@ def test_gpu_extraction_empty_and_count_mismatch(dev):
     from gnn_amd import custom_sparse_ops as cso
 
     lap = _graph("symmetric")
+    ip = lap.indptr.astype(np.int64)
     g = sampler.device_graph(lap, dev)
-    i32 = lambda a: torch.tensor(a, dtype=torch.int32, device=dev)
-    op = cso.extract_operand(g, i32([]), i32([1, 2]), torch.ones(2, device=dev), 0, i32([0, 0, 0]))
+    i32 = lambda a: torch.tensor(np.asarray(a, np.int64), dtype=torch.int32, device=dev)
+    seg = lambda nodes: i32(np.concatenate([[0], np.cumsum(ip[np.asarray(nodes, np.int64) + 1] - ip[np.asarray(nodes, np.int64)])]))
+    op = cso.extract_operand(g, i32([]), i32([1, 2]), torch.ones(2, device=dev), 0, seg([]), seg([1, 2]),
+                             i32([0, 0, 0]))
     assert op.rowptr.tolist() == [0] and op.nnz == 0
-    op = cso.extract_operand(g, i32([3, 4]), i32([]), torch.ones(0, device=dev), 0)
+    assert op.transpose().rowptr.tolist() == [0, 0, 0]
+    op = cso.extract_operand(g, i32([3, 4]), i32([]), torch.ones(0, device=dev), 0, seg([3, 4]))
     assert op.rowptr.tolist() == [0, 0, 0]
     g.check()
     nb = np.asarray(lap[[5, 6]].indices)
     cols = np.unique(nb)[:5].astype(np.int32)
     true_nnz = int(np.isin(lap[[5, 6]].indices, cols).sum())
     op = cso.extract_operand(g, i32([5, 6]), torch.from_numpy(cols).to(dev), torch.ones(cols.size, device=dev),
-                             true_nnz + 1)
+                             true_nnz, seg([5, 6]))
+    torch.cuda.synchronize()
+    g.check()
+    assert op.rowptr[-1].item() == true_nnz
+    op = cso.extract_operand(g, i32([5, 6]), torch.from_numpy(cols).to(dev), torch.ones(cols.size, device=dev),
+                             true_nnz + 1, seg([5, 6]))
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="disagree"):
         g.check()
