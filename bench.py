@@ -88,9 +88,10 @@ def parse():
                     help="non-buffered feature rows: host gather into pinned memory + one hipMemcpyAsync "
                          "(copy), or the GPU reads the mapped host table over PCIe (zerocopy: measured "
                          "slower, it slows the concurrent compute kernels)")
-    ap.add_argument("--host-extract", action="store_true",
-                    help="LADIES: extract every layer's sub-graph on the host (sampler threads) instead of "
-                         "leaving the layers below the top one to the GPU extraction (gnn_ladies_extract_f32)")
+    ap.add_argument("--extract-layers", default="all",
+                    help="LADIES: bottom-up layers (below the top one) whose sub-graph the GPU extracts "
+                         "(gnn_ladies_extract_f32) instead of the sampler threads: comma list, 'all' or 'none'")
+    ap.add_argument("--host-extract", action="store_true", help="= --extract-layers none")
     ap.add_argument("--python-loader", action="store_true",
                     help="batch producer: Python worker threads calling the native sampler (BatchLoader) instead of "
                          "the C++ producer (NativeLoader: GIL-free workers, one blob and one H2D per batch)")
@@ -509,7 +510,12 @@ def main():
     from gnn_amd.loader import BatchLoader, NativeLoader
 
     workers = args.workers or default_workers(world)
-    dx = args.sampler == "ladies" and not args.host_extract
+    if args.sampler != "ladies" or args.host_extract or args.extract_layers == "none":
+        dx = False
+    elif args.extract_layers == "all":
+        dx = True
+    else:
+        dx = [int(v) for v in args.extract_layers.split(",") if v]
     loader = (BatchLoader if args.python_loader else NativeLoader)(
         lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank, world_size=world,
         store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx)
@@ -619,7 +625,7 @@ def main():
         if dx:
             t = time.perf_counter()
             for i, c in enumerate(chunks[:3]):
-                fn(i, c, samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0], device_extract=True)
+                fn(i, c, samp, N, lap, labels, [1, 1, 1], pdev, pidx, None, 1.0, [0], device_extract=dx)
             sampler_cost["native_draw_only_ms_per_batch_1thread"] = round((time.perf_counter() - t) / 3 * 1e3, 1)
             sampler_cost["note"] = ("native: host extraction of every layer; draw_only: the layers below the top "
                                     "one left to the GPU extraction (what the end-to-end run uses)")
@@ -648,7 +654,7 @@ def main():
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
                        "sampler_workers_per_rank": workers,
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
-                       "layer_extraction": "gpu (layers below the top one)" if dx else "host"},
+                       "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,

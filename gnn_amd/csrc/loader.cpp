@@ -414,7 +414,7 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
     ld->samp.assign(samp_num, samp_num + num_layers);
     ld->orders.assign(orders, orders + num_layers);
     ld->kind = kind;
-    ld->device_extract = device_extract && !data;
+    ld->device_extract = data ? 0 : device_extract;
     ld->csc_from = csc_from;
     ld->fastgcn_p = fastgcn_p;
     ld->pool.reset(new Pool(pinned != 0));

@@ -420,7 +420,9 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
       if (orders[num_layers - 1 - d] == 0) continue;         // orders1 = orders[::-1]
       L.present = true;
-      const bool dev = device_extract && !top;  // rows = np.unique(...) of the layer above
+      // below the top layer rows = np.unique(...) of the layer above; device_extract is a mask
+      // over the (bottom-up) layer index, -1 = every layer below the top one
+      const bool dev = !top && ((device_extract >> (num_layers - 1 - d)) & 1);
       top = false;
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
       if (unnz < 0) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");

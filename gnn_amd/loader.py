@@ -78,7 +78,7 @@ class BatchLoader:
     def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
-                 seed: int = 0, devices=None, kind: str = "ladies", device_extract: bool = False):
+                 seed: int = 0, devices=None, kind: str = "ladies", device_extract=False):
         fns = {"ladies": smp.ladies_sample_host, "subgraph": smp.subgraph_sample_host,
                "fastgcn": smp.fastgcn_sample_host}
         if kind not in fns:
@@ -86,7 +86,7 @@ class BatchLoader:
         self.sample_fn = fns[kind]
         # LADIES: leave the layers below the top one to the GPU extraction (to_device), so the
         # worker threads only draw (sampler.ladies_sample_host(device_extract=True))
-        self.kw = {"device_extract": True} if device_extract and kind == "ladies" else {}
+        self.kw = {"device_extract": device_extract} if device_extract and kind == "ladies" else {}
         self.graph = smp.native_graph(lap)
         self.labels = labels_full
         self.train = np.asarray(train_nodes)
@@ -331,7 +331,7 @@ class NativeLoader:
     def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
-                 seed: int = 0, devices=None, kind: str = "ladies", device_extract: bool = False,
+                 seed: int = 0, devices=None, kind: str = "ladies", device_extract=False,
                  pinned: Optional[bool] = None):
         import scipy.sparse as sp
 
@@ -374,7 +374,7 @@ class NativeLoader:
         if pinned is None:
             pinned = torch.cuda.is_available()
         L = _lib.sampler_lib()
-        dx = int(bool(device_extract) and kind == "ladies" and g.data is None)
+        dx = smp.extract_mask(device_extract) if (kind == "ladies" and g.data is None) else 0
         ipt = g.transpose_structure[1] if dx else None
         self.handle = L.gnn_loader_create(
             ptr(g.indptr), ptr(g.indices), ptr(g.data), ptr(ipt), g.num_nodes, ptr(k["lab_ptr"]), ptr(k["lab_idx"]),

@@ -307,13 +307,26 @@ def native_graph(lap) -> NativeGraph:
     return g
 
 
+def extract_mask(device_extract) -> int:
+    """device_extract (True = every layer below the top one, False / None = none, or an iterable
+    of bottom-up layer indices) as the native samplers' layer mask (-1 = all)."""
+    if device_extract is True:
+        return -1
+    if not device_extract:
+        return 0
+    m = 0
+    for li in device_extract:
+        m |= 1 << int(li)
+    return m
+
+
 def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies",
-                   csc_from: int = 1, device_extract: bool = False):
+                   csc_from: int = 1, device_extract=False):
     """Run gnn_ladies_sample / gnn_subgraph_sample / gnn_fastgcn_sample and copy the result
     out: (layers, sampled_nodes, input_nodes, pinned tensors). Layers >= csc_from (those
     whose input needs a gradient; layer 0's input is the features) also get their CSC.
-    device_extract (LADIES): the layers below the top one are left to the GPU extraction —
-    only their rows, columns, CSC column pointer and nnz come back."""
+    device_extract (LADIES; see extract_mask): those layers below the top one are left to the GPU
+    extraction — only their rows, columns, segment offsets, CSC column pointer and nnz come back."""
     import ctypes
 
     from . import _lib
@@ -332,7 +345,7 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
     elif kind == "ladies" and device_extract:
         ipt = graph.transpose_structure[1]
         rc = L.gnn_ladies_sample_dev(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), ptr(ipt), graph.num_nodes,
-                                     *rest[:-1], 1, rest[-1])
+                                     *rest[:-1], extract_mask(device_extract), rest[-1])
     else:
         rc = (L.gnn_ladies_sample if kind == "ladies" else L.gnn_subgraph_sample)(*g3, *rest)
     _lib.check_sampler(rc, f"gnn_{kind}_sample")
@@ -395,20 +408,21 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
 def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
                        orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
                        skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
-                       native: bool = True, device_extract: bool = False) -> HostBatch:
+                       native: bool = True, device_extract=False) -> HostBatch:
     """sampler.py:90-160 without the device work.
 
     native=True runs the C++ sampler (libgnn_sampler.so, bit-identical; releases the GIL, so
     batches sample concurrently on threads); native=False (and scale_factor > 1, a branch the
-    reference never reaches) runs the numpy restatement below. device_extract=True (native, a
-    graph without stored zeros): the layers below the top one are extracted on the GPU by
-    ``to_device`` (gnn_ladies_extract_f32) instead of on the host — same operands."""
+    reference never reaches) runs the numpy restatement below. device_extract (native, a graph
+    without stored zeros; True = every layer below the top one, or bottom-up layer indices):
+    those layers are extracted on the GPU by ``to_device`` (gnn_ladies_extract_f32) instead of on
+    the host — same operands."""
     batch_nodes = np.asarray(batch_nodes)
     if native and not scale_factor > 1:
         g = native_graph(lap_matrix)
         if g.num_nodes != num_nodes:
             raise ValueError("num_nodes does not match lap_matrix")
-        dx = bool(device_extract) and g.data is None
+        dx = device_extract if (extract_mask(device_extract) and g.data is None) else False
         layers, sampled_nodes, previous_nodes, pinned = _native_layers(seed, batch_nodes, samp_num_list, g,
                                                                        list(orders), device_extract=dx)
         hb = _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,

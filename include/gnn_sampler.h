@@ -41,9 +41,9 @@ int gnn_ladies_sample(const int64_t* indptr, const int32_t* indices, const float
                       const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                       const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
 
-/* Same draw (bit-identical RNG stream, sampled nodes, normfact), with device_extract != 0: every
- * layer below the top one (its rows are the ascending, unique `after` of the layer above) is NOT
- * extracted on the host — the host keeps only what the draw needs (U's column counts) and records
+/* Same draw (bit-identical RNG stream, sampled nodes, normfact), with device_extract a mask over
+ * the bottom-up layer index (-1: all): every selected layer below the top one (its rows are the
+ * ascending, unique `after` of the layer above) is NOT extracted on the host — the host keeps only what the draw needs (U's column counts) and records
  * the layer's rows, columns, exact nnz and CSC column pointer for gnn_ladies_extract_f32
  * (include/gnn_extract.h), which builds adj = U[:, after] and its transpose on the GPU from the
  * graph resident there. Requires data == NULL (no stored zeros: the column counts are then the

@@ -169,3 +169,39 @@ def test_gpu_extraction_empty_and_count_mismatch(dev):
     with pytest.raises(RuntimeError, match="disagree"):
         g.check()
     g.err.zero_()
+
+
+def test_extract_layer_mask():
+    """device_extract as bottom-up layer indices: only those layers go to the GPU; the others
+    keep the host extraction (and CSC) of the plain sampler, the draw is unchanged."""
+    lap = _graph("symmetric")
+    N = lap.shape[0]
+    batch = np.random.default_rng(7).choice(N, 128, replace=False)
+    args = (13, batch, np.array([500] * 3), N, lap, _labels(N), [1, 1, 1], np.full(N, -1), np.zeros(N, np.int64),
+            None, 1.0, [0])
+    hb = sampler.ladies_sample_host(*args)
+    for mask, on in (([0], [True, False, False]), ([1], [False, True, False]), ([], [False, False, False])):
+        hd = sampler.ladies_sample_host(*args, device_extract=mask)
+        assert [L.on_device for L in hd.layers] == on
+        for L, D in zip(hb.layers, hd.layers):
+            assert np.array_equal(L.normfact, D.normfact) and L.nnz == D.nnz
+            if not D.on_device:
+                assert np.array_equal(L.colidx, D.colidx) and np.array_equal(L.rowptr, D.rowptr)
+
+
+@pytest.mark.gpu
+def test_gpu_extraction_layer_mask(dev):
+    lap = _graph("symmetric")
+    N = lap.shape[0]
+    batch = np.random.default_rng(8).choice(N, 128, replace=False)
+    args = (17, batch, np.array([500] * 3), N, lap, _labels(N), [1, 1, 1], np.full(N, -1), np.zeros(N, np.int64),
+            None, 1.0, [0])
+    db = sampler.ladies_sample_host(*args).to_device(dev, with_coo=False)
+    dd = sampler.ladies_sample_host(*args, device_extract=[0]).to_device(dev, with_coo=False)
+    for li, (a, b) in enumerate(zip(db.adjs, dd.adjs)):
+        for k in ("rowptr", "col", "val"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), (li, k)
+        if li >= 1:
+            for k in ("rowptr", "col", "val"):
+                assert torch.equal(getattr(a.transpose(), k), getattr(b.transpose(), k)), (li, "t", k)
+    dd.graph.check()
