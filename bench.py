@@ -525,6 +525,8 @@ def main():
         sampler.device_graph(loader.graph, dev)
         torch.cuda.synchronize()
     it = loader.forever()
+    if exchange is not None:  # each batch's peer negotiation off the training thread, 4 batches ahead
+        it = staging.NegotiatedStream(it, exchange, depth=4)
 
     def nxt_live():
         lb = next(it)

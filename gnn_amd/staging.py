@@ -115,6 +115,7 @@ class StagePlan:
     peer_src: List[np.ndarray]   # per peer rank: slots in that peer's buffer
     pinned: tuple = ()           # pinned host copies of (own_pos, own_src, host_pos[, host_src])
     blob: object = None          # a loader.NativeBatch: every array above lives in its blob, uploaded once
+    peer_meta: object = None     # a Future of PeerExchange.prepare(plan), negotiated ahead (NegotiatedStream)
 
 
 def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devices=None) -> StagePlan:
@@ -169,8 +170,14 @@ class Stager:
         meta = None
         if self.exchange is not None:
             # host-side metadata all-to-all (gloo), in batch order, paid for every issue: the
-            # negotiation is part of each step (never cached on a plan that is issued again)
-            meta = self.exchange.prepare(plan)
+            # negotiation is part of each step (never cached on a plan that is issued again) —
+            # made ahead on the NegotiatedStream's thread when the batch came through one
+            fut = plan.peer_meta
+            if fut is not None:
+                plan.peer_meta = None
+                meta = fut.result()
+            else:
+                meta = self.exchange.prepare(plan)
         # No wait on the compute stream: staging only reads static buffers and its own
         # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
@@ -265,6 +272,44 @@ class Retirement:
         while self.q:
             ev0, _ = self.q.popleft()
             ev0.synchronize()
+
+
+class NegotiatedStream:
+    """Wraps a stream of loader batches (LoadedBatch) and runs each batch's peer negotiation
+    (PeerExchange.prepare: two gloo all-to-alls of request sizes and slot ids) on ONE background
+    thread, ``depth`` batches ahead of the consumer, so the training thread never blocks on the
+    other ranks' hosts inside a step. Every rank pulls the same number of batches (consumed +
+    depth), so the collectives pair up in batch order across ranks; only this thread uses the
+    metadata group."""
+
+    def __init__(self, it, exchange: "PeerExchange", depth: int = 4):
+        import collections
+        from concurrent.futures import ThreadPoolExecutor
+
+        self.it = iter(it)
+        self.exchange = exchange
+        self.depth = max(0, int(depth))
+        self.q = collections.deque()
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="gnn-peer-meta")
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        while self.it is not None and len(self.q) <= self.depth:
+            try:
+                lb = next(self.it)
+            except StopIteration:
+                self.it = None
+                break
+            lb.plan.peer_meta = self.pool.submit(self.exchange.prepare, lb.plan)
+            self.q.append(lb)
+        if not self.q:
+            raise StopIteration
+        return self.q.popleft()
+
+    def close(self):
+        self.pool.shutdown(wait=True)
 
 
 class PeerExchange:

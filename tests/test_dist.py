@@ -108,6 +108,37 @@ def _exchange_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _negotiated_worker(rank, world, port, q):
+    """NegotiatedStream: the metadata negotiated ahead on its thread equals the synchronous
+    PeerExchange.prepare of the same batches, in order."""
+    _init(rank, world, port)
+    from gnn_amd import loader, staging
+
+    rng = np.random.default_rng(10 + rank)
+    plans = []
+    for b in range(7):
+        peer_pos = [np.zeros(0, np.int64)] * world
+        peer_src = [np.zeros(0, np.int64)] * world
+        n = int(rng.integers(0, 6))
+        peer_pos[1 - rank] = np.sort(rng.choice(20, n, replace=False)).astype(np.int64)
+        peer_src[1 - rank] = rng.integers(0, 50, n).astype(np.int64)
+        plans.append(staging.StagePlan(20, np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.int64),
+                                       None, peer_pos, peer_src))
+    ex = staging.PeerExchange()
+    ref = [ex.prepare(p) for p in plans]
+    stream = staging.NegotiatedStream((loader.LoadedBatch(None, p) for p in plans), ex, depth=3)
+    ok = True
+    n = 0
+    for i, lb in enumerate(stream):
+        n += 1
+        got = lb.plan.peer_meta.result()
+        ok &= got[0] == ref[i][0] and got[1] == ref[i][1]
+        ok &= torch.equal(got[2], ref[i][2]) and torch.equal(got[3], ref[i][3])
+    stream.close()
+    q.put((rank, bool(ok) and n == len(plans)))
+    dist.destroy_process_group()
+
+
 def _spawn(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -131,4 +162,9 @@ def test_trainer_allreduce_matches_thread_sum():
 
 def test_peer_exchange_rows():
     out = _spawn(_exchange_worker)
+    assert all(ok for _, ok in out)
+
+
+def test_negotiated_stream_matches_prepare():
+    out = _spawn(_negotiated_worker)
     assert all(ok for _, ok in out)
