@@ -332,7 +332,10 @@ class PeerExchange:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         if meta_group is None:
-            meta_group = group if dist.get_backend(group) == "gloo" else dist.new_group(backend="gloo")
+            # always a group of its own: the negotiation may run on another thread
+            # (NegotiatedStream) while this thread's row all-to-all / gradient all-reduce use
+            # `group` — two threads on one communicator would interleave their collectives
+            meta_group = dist.new_group(backend="gloo")
         self.meta_group = meta_group
 
     def prepare(self, plan: StagePlan) -> tuple:
