@@ -71,6 +71,9 @@ _SIGNATURES = {
     "gnn_ladies_extract_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int32]),
     "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP,
                                       _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
+    # include/gnn_step.h
+    "gnn_train_step_workspace_bytes": (_SZ, [_VP]),
+    "gnn_train_step_f32": (_INT, [_VP, _VP, _SZ, _VP]),
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
     "gnn_gemm_f32_split3_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),

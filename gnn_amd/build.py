@@ -9,8 +9,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("spmm.hip", "sage.hip", "gemm.hip", "optim.hip", "head.hip", "extract.hip")]
-HDRS = [os.path.join(REPO, "include", f) for f in ("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h")] + [
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("spmm.hip", "sage.hip", "gemm.hip", "optim.hip", "head.hip", "extract.hip", "step.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h", "gnn_step.h")] + [
     os.path.join(HERE, "csrc", "common.h")]
 OUT = os.path.join(HERE, "libgnn_spmm.so")
 ARCH = os.environ.get("GNN_OFFLOAD_ARCH", "gfx950")
@@ -33,7 +33,7 @@ def build_library(force: bool = False, verbose: bool = False) -> str:
                 return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           f"-I{os.path.join(REPO, 'include')}", f'-DGNN_BUILD_ID="{bid}"', "-o", OUT + ".tmp"] + SRCS
+           f"-I{os.path.join(REPO, 'include')}", f'-DGNN_BUILD_ID="{bid}"', "-o", OUT + ".tmp"] + SRCS + ["-lrocblas"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,373 @@
+// step.hip — native executor of one GraphSAGE / GCN training step's forward + backward
+// (include/gnn_step.h).
+//
+// Reference (main.py:122-146): output = model(x0, adjs, sampled_nodes); loss = utils.loss(...);
+// loss.backward() — GraphSageConvolution / GraphConvolution (models.py:6-64) per layer, GNN's
+// head (models.py:86-97) and the BCE loss (utils.py:129-140), autograd for the backward.
+//
+// The Python path (gnn_amd.models fused=True) already runs every piece as a hand-written HIP
+// kernel, but through ~45 autograd Functions and ctypes calls per step: 1.2-1.5 ms of host time
+// against a 1.8 ms GPU step. This executor issues the same kernel sequence from C++ — one
+// call per step, every intermediate carved from one caller-provided workspace — with the same
+// numerics: the same kernels with the same arguments and routing (the split3 GEMM where its
+// tiles fill the chip, the vendor GEMM (rocBLAS) for the small products), the same dropout
+// seeds. Only the two products torch would run through its own reduction (the head's bias
+// gradient, a column sum) use a fixed-order kernel here.
+//
+// Sequence (L layers, bottom-up index l; layer 0's input is the features, so it has no input
+// gradient):
+//   forward  l = 0..L-1:  feat = A_l·X (gnn_spmm_csr_f32);  [SAGE] xs = X[sampled] (row gather)
+//                         [hB,] hW = [xs, feat]·[W_B, W_W]ᵀ  (one batched split3 launch or rocBLAS)
+//                         Y_l = sage_norm(hB + b_B, hW + b_W)  (ELU, row standardise, scale/offset, dropout)
+//   head:                 loss, z = BCE(linear(dropout(normalize(Y_{L-1}))))
+//   backward head:        dz, dY_{L-1};  dW_h = dzᵀ·xd (rocBLAS), db_h = colsum(dz)
+//   backward l = L-1..0:  dhB, dhW, dscale, doffset, dbB, dbW = sage_norm_bwd(dY_l)
+//                         dW_B, dW_W = [dhB, dhW]ᵀ·[xs, feat]  (split-k split3 from 2048 rows)
+//                         l >= 1: dxs, dfeat = [dhB, dhW]·[W_B, W_W];
+//                                 dY_{l-1} = A_lᵀ·dfeat (+ dxs scattered through rmap, SAGE)
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+
+#include "common.h"
+#include "gnn_layers.h"
+#include "gnn_spmm.h"
+#include "gnn_step.h"
+
+namespace {
+
+using gnn::align_up;
+using gnn::ceil_div;
+
+// db = Σ_rows dz (M x C, row-major): one thread per column, rows in order (deterministic).
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ dz, int M, int C,
+                                                     float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.0f;
+  for (int r = 0; r < M; ++r) s += dz[(int64_t)r * C + c];
+  out[c] = s;
+}
+
+// A bump allocator over the workspace; with base == nullptr it only measures.
+struct Arena {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(int64_t count) {
+    const size_t bytes = align_up((size_t)(count > 0 ? count : 1) * sizeof(T), 256);
+    T* p = base ? (T*)(base + off) : nullptr;
+    off += bytes;
+    return p;
+  }
+};
+
+int64_t L(const int64_t* d, int l, int f) { return d[GNN_STEP_HEADER + l * GNN_STEP_LAYER_SLOTS + f]; }
+template <typename T>
+T* P(const int64_t* d, int l, int f) {
+  return (T*)(uintptr_t)L(d, l, f);
+}
+template <typename T>
+T* HP(const int64_t* d, int f) {
+  return (T*)(uintptr_t)d[f];
+}
+
+// The split3 GEMM takes an unsplit product when its 128 x 128 tiles cover the CUs
+// (gnn_amd/fused.py _mfma_fills) and every operand meets its contract (_gemm_ok).
+bool fills(int64_t M, int64_t N, int n) { return ceil_div(M, 128) * ceil_div(N, 128) * n >= 256; }
+bool gemm_ok(const void* p, int64_t ld) { return ((uintptr_t)p % 8) == 0 && (ld % 2) == 0; }
+
+std::mutex g_blas_mu;
+rocblas_handle g_blas[64] = {};
+
+int blas_handle(rocblas_handle* h) {
+  int dev = 0;
+  GNN_HIP(hipGetDevice(&dev), "hipGetDevice");
+  GNN_REQUIRE(dev >= 0 && dev < 64, "gnn_train_step: device index %d", dev);
+  std::lock_guard<std::mutex> g(g_blas_mu);
+  if (!g_blas[dev]) {
+    if (rocblas_create_handle(&g_blas[dev]) != rocblas_status_success)
+      return gnn::fail(-1, "rocblas_create_handle failed");
+  }
+  *h = g_blas[dev];
+  return 0;
+}
+
+// Row-major products on rocBLAS (column-major underneath): the small layer-2 / head products.
+int sgemm(rocblas_handle h, rocblas_operation ta, rocblas_operation tb, int64_t m, int64_t n, int64_t k,
+          const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc) {
+  const float one = 1.0f, zero = 0.0f;
+  if (rocblas_sgemm(h, ta, tb, (rocblas_int)m, (rocblas_int)n, (rocblas_int)k, &one, A, (rocblas_int)lda, B,
+                    (rocblas_int)ldb, &zero, C, (rocblas_int)ldc) != rocblas_status_success)
+    return gnn::fail(-1, "rocblas_sgemm failed (m %lld n %lld k %lld)", (long long)m, (long long)n, (long long)k);
+  return 0;
+}
+// out (M x N) = x (M x K) · Wᵀ (W: N x K)
+int mm_xwt(rocblas_handle h, const float* x, int64_t ldx, const float* W, int64_t ldw, float* out, int64_t ldo,
+           int64_t M, int64_t N, int64_t K) {
+  return sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, W, ldw, x, ldx, out, ldo);
+}
+// out (M x K) = g (M x N) · W (N x K)
+int mm_gw(rocblas_handle h, const float* g, int64_t ldg, const float* W, int64_t ldw, float* out, int64_t ldo,
+          int64_t M, int64_t K, int64_t N) {
+  return sgemm(h, rocblas_operation_none, rocblas_operation_none, K, M, N, W, ldw, g, ldg, out, ldo);
+}
+// out (N x K) = gᵀ (g: M x N) · x (M x K)
+int mm_gtx(rocblas_handle h, const float* g, int64_t ldg, const float* x, int64_t ldx, float* out, int64_t ldo,
+           int64_t N, int64_t K, int64_t M) {
+  return sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, N, M, x, ldx, g, ldg, out, ldo);
+}
+
+// The per-layer buffers of one step (carved in a fixed order: sizing and running share it).
+struct LayerBufs {
+  int64_t M, K, nnz, F, Fk, ldx, ldo, N, D;
+  const float* X;
+  float *feat, *xs, *hB, *hW, *Y, *mean, *rstd;
+  float *dY, *dhB, *dhW, *dxs, *dfeat;
+  void *ws_fwd, *ws_bwd, *ws_norm, *ws_gemm_f, *ws_gemm_dx, *ws_gemm_dw;
+  size_t b_fwd, b_bwd, b_norm, b_gemm_f, b_gemm_dx, b_gemm_dw;
+};
+
+struct Plan {
+  int nl = 0, sage = 1;
+  LayerBufs lb[GNN_STEP_MAX_LAYERS];
+  float *xd, *z, *nrm, *rowloss, *dz, *dXh;
+  int64_t Mh = 0, Dh = 0, C = 0;
+};
+
+int plan(const int64_t* d, Arena& ar, Plan& pl) {
+  GNN_REQUIRE(d[GNN_SH_VERSION] == GNN_STEP_VERSION, "gnn_train_step: descriptor version %lld",
+              (long long)d[GNN_SH_VERSION]);
+  pl.nl = (int)d[GNN_SH_LAYERS];
+  pl.sage = d[GNN_SH_KIND] == GNN_STEP_SAGE;
+  GNN_REQUIRE(pl.nl >= 1 && pl.nl <= GNN_STEP_MAX_LAYERS, "gnn_train_step: %d layers", pl.nl);
+  const int64_t N = d[GNN_SH_NHID];
+  const int n = pl.sage ? 2 : 1;
+  for (int l = 0; l < pl.nl; ++l) {
+    LayerBufs& b = pl.lb[l];
+    b.M = L(d, l, GNN_SL_M);
+    b.K = L(d, l, GNN_SL_K);
+    b.nnz = L(d, l, GNN_SL_NNZ);
+    b.N = N;
+    b.D = n * N;
+    if (l == 0) {
+      b.X = HP<const float>(d, GNN_SH_X0);
+      b.ldx = d[GNN_SH_LDX0];
+      b.F = d[GNN_SH_F0];
+    } else {
+      const LayerBufs& p = pl.lb[l - 1];
+      GNN_REQUIRE(b.K == p.M, "gnn_train_step: layer %d has K = %lld, layer %d M = %lld", l, (long long)b.K, l - 1,
+                  (long long)p.M);
+      b.X = p.Y;
+      b.ldx = p.D;
+      b.F = p.D;
+    }
+    GNN_REQUIRE(b.F <= b.ldx && b.F > 0 && b.M > 0 && b.K > 0, "gnn_train_step: layer %d shape", l);
+    // the aggregation's padded width (custom_sparse_ops.spmm_csr): 16-byte loads over whole
+    // line-aligned rows when the input rows are padded (the 602-wide features in 608-float rows)
+    b.Fk = b.F;
+    if (b.F % 4 && b.ldx % 4 == 0 && ((uintptr_t)b.X % 16 == 0 || !ar.base) && b.ldx >= b.F + (4 - b.F % 4))
+      b.Fk = b.F + (4 - b.F % 4);
+    b.ldo = (b.Fk != b.F && b.ldx <= 2 * b.Fk) ? b.ldx : b.Fk;
+    b.feat = ar.take<float>(b.M * b.ldo);
+    b.xs = pl.sage ? ar.take<float>(b.M * b.ldo) : nullptr;
+    b.hB = pl.sage ? ar.take<float>(b.M * N) : nullptr;
+    b.hW = ar.take<float>(b.M * N);
+    b.Y = ar.take<float>(b.M * b.D);
+    b.mean = ar.take<float>(b.M);
+    b.rstd = ar.take<float>(b.M);
+    b.b_fwd = gnn_spmm_workspace_bytes(b.M, b.nnz, b.Fk, 0);
+    b.ws_fwd = ar.take<char>((int64_t)b.b_fwd);
+    b.b_gemm_f = gnn_gemm_f32_split3_workspace_bytes(b.M, N, b.F, n);
+    b.ws_gemm_f = ar.take<char>((int64_t)b.b_gemm_f);
+  }
+  const LayerBufs& top = pl.lb[pl.nl - 1];
+  pl.Mh = top.M;
+  pl.Dh = top.D;
+  pl.C = d[GNN_SH_CLASSES];
+  GNN_REQUIRE(pl.C > 0 && pl.C <= 64 && pl.Dh % 4 == 0 && pl.Dh <= 2048, "gnn_train_step: head %lld x %lld",
+              (long long)pl.Dh, (long long)pl.C);
+  pl.xd = ar.take<float>(pl.Mh * pl.Dh);
+  pl.z = ar.take<float>(pl.Mh * pl.C);
+  pl.nrm = ar.take<float>(pl.Mh);
+  pl.rowloss = ar.take<float>(pl.Mh);
+  pl.dz = ar.take<float>(pl.Mh * pl.C);
+  pl.dXh = ar.take<float>(pl.Mh * pl.Dh);
+  for (int l = pl.nl - 1; l >= 0; --l) {
+    LayerBufs& b = pl.lb[l];
+    b.dY = (l == pl.nl - 1) ? pl.dXh : pl.lb[l + 1].dfeat;  // placeholder, set below for l < nl-1
+    b.dhB = pl.sage ? ar.take<float>(b.M * N) : nullptr;
+    b.dhW = ar.take<float>(b.M * N);
+    b.b_norm = gnn_sage_norm_bwd_workspace_bytes(b.M, b.D);
+    b.ws_norm = ar.take<char>((int64_t)b.b_norm);
+    b.b_gemm_dw = gnn_gemm_f32_split3_workspace_bytes(N, b.F, b.M, n);
+    b.ws_gemm_dw = ar.take<char>((int64_t)b.b_gemm_dw);
+    if (l >= 1) {
+      b.dxs = pl.sage ? ar.take<float>(b.M * b.F) : nullptr;
+      b.dfeat = ar.take<float>(b.M * b.F);
+      b.b_gemm_dx = gnn_gemm_f32_split3_workspace_bytes(b.M, b.F, N, n);
+      b.ws_gemm_dx = ar.take<char>((int64_t)b.b_gemm_dx);
+      b.b_bwd = gnn_spmm_workspace_bytes(b.K, b.nnz, b.F, 0);
+      b.ws_bwd = ar.take<char>((int64_t)b.b_bwd);
+    } else {
+      b.dxs = b.dfeat = nullptr;
+      b.ws_gemm_dx = b.ws_bwd = nullptr;
+      b.b_gemm_dx = b.b_bwd = 0;
+    }
+  }
+  // dY of layer l < nl-1 is the input gradient of layer l+1 (K_{l+1} x F_{l+1} = M_l x D_l)
+  for (int l = 0; l < pl.nl - 1; ++l) pl.lb[l].dY = ar.take<float>(pl.lb[l].M * pl.lb[l].D);
+  return 0;
+}
+
+#define GNN_TRY(x)        \
+  do {                    \
+    int rc_ = (x);        \
+    if (rc_) return rc_;  \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+size_t gnn_train_step_workspace_bytes(const int64_t* desc) {
+  if (!desc) return 0;
+  Arena ar{nullptr};
+  Plan pl;
+  if (plan(desc, ar, pl)) return 0;
+  return ar.off;
+}
+
+int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes, void* stream) {
+  GNN_REQUIRE(d != nullptr, "gnn_train_step: NULL descriptor");
+  Arena ar{(char*)workspace};
+  Plan pl;
+  {
+    Arena dry{nullptr};
+    Plan tmp;
+    GNN_TRY(plan(d, dry, tmp));
+    GNN_REQUIRE(workspace && workspace_bytes >= dry.off, "gnn_train_step: workspace too small (%zu < %zu)",
+                workspace_bytes, dry.off);
+    GNN_REQUIRE((uintptr_t)workspace % 256 == 0, "gnn_train_step: workspace not 256-byte aligned");
+  }
+  GNN_TRY(plan(d, ar, pl));
+  hipStream_t st = (hipStream_t)stream;
+  rocblas_handle h = nullptr;
+  GNN_TRY(blas_handle(&h));
+  if (rocblas_set_stream(h, st) != rocblas_status_success) return gnn::fail(-1, "rocblas_set_stream failed");
+  const int n = pl.sage ? 2 : 1;
+  const float p = [&] {
+    float f;
+    const int32_t bits = (int32_t)d[GNN_SH_PDROP_BITS];
+    std::memcpy(&f, &bits, 4);
+    return f;
+  }();
+  const int training = (int)d[GNN_SH_TRAINING];
+  // ------------------------------------------------------------------ forward
+  for (int l = 0; l < pl.nl; ++l) {
+    LayerBufs& b = pl.lb[l];
+    const int64_t N = b.N;
+    GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                             P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                             b.ws_fwd, b.b_fwd, 0, st));
+    const float* WB = P<const float>(d, l, GNN_SL_WB);
+    const float* WW = P<const float>(d, l, GNN_SL_WW);
+    if (pl.sage) {
+      GNN_REQUIRE(L(d, l, GNN_SL_NSAMPLED) == b.M, "gnn_train_step: layer %d sampled %lld != M %lld", l,
+                  (long long)L(d, l, GNN_SL_NSAMPLED), (long long)b.M);
+      GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M, b.F,
+                                  st));
+    }
+    const bool ok = gemm_ok(b.feat, b.ldo) && gemm_ok(WW, b.F) && (!pl.sage || gemm_ok(WB, b.F));
+    if (ok && fills(b.M, N, n)) {
+      const float* A[2] = {pl.sage ? b.xs : b.feat, b.feat};
+      const float* B[2] = {pl.sage ? WB : WW, WW};
+      float* Cc[2] = {pl.sage ? b.hB : b.hW, b.hW};
+      GNN_TRY(gnn_gemm_f32_split3(0, 0, b.M, N, b.F, n, A + (pl.sage ? 0 : 1), b.ldo, B + (pl.sage ? 0 : 1), b.F,
+                                  Cc + (pl.sage ? 0 : 1), N, b.ws_gemm_f, b.b_gemm_f, st));
+    } else {
+      if (pl.sage) GNN_TRY(mm_xwt(h, b.xs, b.ldo, WB, b.F, b.hB, N, b.M, N, b.F));
+      GNN_TRY(mm_xwt(h, b.feat, b.ldo, WW, b.F, b.hW, N, b.M, N, b.F));
+    }
+    GNN_TRY(gnn_sage_norm_fwd_f32(pl.sage ? b.hB : nullptr, pl.sage ? N : 4, pl.sage ? N : 0, b.hW, N, N,
+                                  pl.sage ? P<const float>(d, l, GNN_SL_BB) : nullptr, P<const float>(d, l, GNN_SL_BW),
+                                  P<const float>(d, l, GNN_SL_SCALE), P<const float>(d, l, GNN_SL_OFFSET), b.M, p,
+                                  (uint64_t)L(d, l, GNN_SL_SEED), training, b.Y, b.D, b.mean, b.rstd, st));
+  }
+  // ------------------------------------------------------------------ head + loss
+  const LayerBufs& top = pl.lb[pl.nl - 1];
+  const float* Wh = HP<const float>(d, GNN_SH_HEAD_W);
+  const uint64_t hseed = (uint64_t)d[GNN_SH_HEAD_SEED];
+  const float* labels = HP<const float>(d, GNN_SH_LABELS);
+  const int64_t ldl = d[GNN_SH_LDL];
+  GNN_TRY(gnn_head_bce_fwd_f32(top.Y, top.D, pl.Mh, pl.Dh, Wh, HP<const float>(d, GNN_SH_HEAD_B), pl.C, labels, ldl, p,
+                               hseed, training, pl.xd, pl.z, pl.nrm, pl.rowloss, HP<float>(d, GNN_SH_LOSS), st));
+  // ------------------------------------------------------------------ backward
+  GNN_TRY(gnn_head_bce_bwd_f32(top.Y, top.D, pl.Mh, pl.Dh, Wh, pl.C, labels, ldl, nullptr, p, hseed, training, pl.z,
+                               pl.nrm, pl.dz, pl.dXh, pl.Dh, st));
+  GNN_TRY(mm_gtx(h, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
+  if (HP<float>(d, GNN_SH_HEAD_GB)) {
+    colsum_kernel<<<dim3((unsigned)ceil_div(pl.C, 256)), dim3(256), 0, st>>>(pl.dz, (int)pl.Mh, (int)pl.C,
+                                                                           HP<float>(d, GNN_SH_HEAD_GB));
+    GNN_LAUNCHED("colsum_kernel");
+  }
+  for (int l = pl.nl - 1; l >= 0; --l) {
+    LayerBufs& b = pl.lb[l];
+    const int64_t N = b.N;
+    const float* WB = P<const float>(d, l, GNN_SL_WB);
+    const float* WW = P<const float>(d, l, GNN_SL_WW);
+    GNN_TRY(gnn_sage_norm_bwd_f32(b.dY, b.D, pl.sage ? b.hB : nullptr, pl.sage ? N : 4, pl.sage ? N : 0, b.hW, N, N,
+                                  pl.sage ? P<const float>(d, l, GNN_SL_BB) : nullptr, P<const float>(d, l, GNN_SL_BW),
+                                  P<const float>(d, l, GNN_SL_SCALE), b.mean, b.rstd, b.M, p,
+                                  (uint64_t)L(d, l, GNN_SL_SEED), training, b.dhB, b.dhW, P<float>(d, l, GNN_SL_GSCALE),
+                                  P<float>(d, l, GNN_SL_GOFFSET), pl.sage ? P<float>(d, l, GNN_SL_GBB) : nullptr,
+                                  P<float>(d, l, GNN_SL_GBW), b.ws_norm, b.b_norm, st));
+    const bool ok = gemm_ok(b.feat, b.ldo) && gemm_ok(WW, b.F) && (!pl.sage || gemm_ok(WB, b.F));
+    const float* G[2] = {pl.sage ? b.dhB : b.dhW, b.dhW};
+    const int o = pl.sage ? 0 : 1;
+    if (l >= 1) {  // input gradients (layer 0's input is the features)
+      if (ok && fills(b.M, b.F, n)) {
+        const float* B[2] = {pl.sage ? WB : WW, WW};
+        float* Cc[2] = {pl.sage ? b.dxs : b.dfeat, b.dfeat};
+        GNN_TRY(gnn_gemm_f32_split3(0, 1, b.M, b.F, N, n, G + o, N, B + o, b.F, Cc + o, b.F, b.ws_gemm_dx,
+                                    b.b_gemm_dx, st));
+      } else {
+        if (pl.sage) GNN_TRY(mm_gw(h, b.dhB, N, WB, b.F, b.dxs, b.F, b.M, b.F, N));
+        GNN_TRY(mm_gw(h, b.dhW, N, WW, b.F, b.dfeat, b.F, b.M, b.F, N));
+      }
+    }
+    // weight gradients: split over the sampled rows on split3 from 2048 rows, else rocBLAS
+    float* gWB = pl.sage ? P<float>(d, l, GNN_SL_GWB) : nullptr;
+    float* gWW = P<float>(d, l, GNN_SL_GWW);
+    if (ok && b.M >= 2048) {
+      const float* X[2] = {pl.sage ? b.xs : b.feat, b.feat};
+      float* Cc[2] = {pl.sage ? gWB : gWW, gWW};
+      GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
+                                  b.b_gemm_dw, st));
+    } else {
+      if (pl.sage) GNN_TRY(mm_gtx(h, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
+      GNN_TRY(mm_gtx(h, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
+    }
+    if (l >= 1) {  // dY_{l-1} = A_lᵀ·dfeat (+ dxs through rmap: the x[sampled] gradient)
+      LayerBufs& prev = pl.lb[l - 1];
+      GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_TROWPTR) != nullptr, "gnn_train_step: layer %d has no transpose", l);
+      if (pl.sage) {
+        GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_RMAP) != nullptr, "gnn_train_step: layer %d has no row map", l);
+        GNN_TRY(gnn_spmm_csr_f32_ex(P<const int32_t>(d, l, GNN_SL_TROWPTR), P<const int32_t>(d, l, GNN_SL_TCOL),
+                                    P<const float>(d, l, GNN_SL_TVAL), b.K, b.M, b.nnz, b.dfeat, b.F, prev.dY, b.F,
+                                    b.F, b.dxs, b.F, P<const int32_t>(d, l, GNN_SL_RMAP), b.ws_bwd, b.b_bwd, 0, st));
+      } else {
+        GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_TROWPTR), P<const int32_t>(d, l, GNN_SL_TCOL),
+                                 P<const float>(d, l, GNN_SL_TVAL), b.K, b.M, b.nnz, b.dfeat, b.F, prev.dY, b.F, b.F,
+                                 b.ws_bwd, b.b_bwd, 0, st));
+      }
+    }
+  }
+  return 0;
+}
+
+}  // extern "C"

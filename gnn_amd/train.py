@@ -44,6 +44,17 @@ class Trainer:
             self.optimizer = ClipAdam(self.params, lr=lr, max_norm=clip)
         else:
             self.optimizer = torch.optim.Adam(self.params, lr=lr)
+        # the whole forward + backward as one native call when the model allows it
+        # (gnn_amd.executor, include/gnn_step.h); GNN_NATIVE_STEP=0 keeps the autograd path
+        self.executor = None
+        if self.native:
+            from . import executor as ex
+
+            if ex.enabled():
+                try:
+                    self.executor = ex.NativeStep(model)
+                except ValueError:
+                    self.executor = None
         self.world = 1
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world = torch.distributed.get_world_size(group)
@@ -73,10 +84,19 @@ class Trainer:
         return flat
 
     def step(self, x0, adjs, sampled_nodes, labels) -> torch.Tensor:
-        for p in self.params:
-            p.grad = None
         if not self.model.training:  # module.train() walks every submodule: ~50 µs of host time
             self.model.train()
+        if self.executor is not None and self.executor.supports(x0, adjs, sampled_nodes, labels):
+            loss = self.executor.step(x0, adjs, sampled_nodes, labels)  # grads into the flat buffer
+            if self.world > 1:
+                flat = self.optimizer.clip_to_flat()
+                torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
+                self.optimizer.step(clipped=True)
+            else:
+                self.optimizer.step()
+            return loss
+        for p in self.params:
+            p.grad = None
         if hasattr(self.model, "forward_loss"):
             loss, _ = self.model.forward_loss(x0, adjs, sampled_nodes, labels, self.sigmoid_loss)
         else:
