@@ -106,6 +106,9 @@ class NativeStep:
         if not (x0.is_cuda and x0.dtype == torch.float32 and x0.stride(1) == 1 and labels.dtype == torch.float32
                 and labels.dim() == 2 and labels.stride(1) == 1):
             return False
+        C, D = self.model.linear.weight.shape
+        if C > 64 or D % 4 or D > 2048 or labels.shape[1] != C:  # the fused head's contract (fused.head_supported)
+            return False
         for li, op in enumerate(adjs):
             if not isinstance(op, CsrOperand):
                 return False
