@@ -12,6 +12,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <emmintrin.h>
 #include <memory>
 #include <new>
 #include <string>
@@ -86,39 +87,88 @@ class MT19937 {
 // `rand(size - n_uniq)` draws, p of the already found entries zeroed, cdf = cumsum(p) /
 // cdf[-1], searchsorted(side='right'), de-duplicated in first-occurrence order.
 // cumsum over the zero entries adds +0.0 (exact) and searchsorted('right') never lands on a
-// zero-probability index, so both run over the ascending list of currently non-zero
-// entries `live` with identical results.
-template <class Prob>
-void choice_without_replacement(MT19937& rng, Prob prob, std::vector<int64_t> live, int64_t size,
-                                std::vector<uint8_t>& taken, std::vector<int64_t>& found) {
+// zero-probability index, so both run over the ascending list of non-zero entries live[0..n)
+// (pv[i] = p[live[i]]) with identical results. Three more exact shortcuts:
+//  - the cdf is never divided: the search compares x against cdf[j] / last at its probe points
+//    only (the same correctly rounded quotient numpy stores, so the same comparisons);
+//  - a round's cumsum is recomputed only from the first position whose p changed (the smallest
+//    index found in the previous round): the prefix below it sums the same terms in the same
+//    order, so it is bit-identical;
+//  - base is cumsum(pv) with nothing taken: the first round reads it, later rounds write their
+//    suffixes to `work` (cdf[i] = i < wfrom ? base[i] : work[i]); FastGCN's base is shared by
+//    every call over the same p, LADIES' is computed with pv in one pass (base == work).
+// The searches of a round run kSearchLanes at a time, branch-free and in lock step, so their
+// cache misses overlap. pv_mutable: found entries' pv is zeroed in place (a per-call pv);
+// otherwise taken[] stands in for the zeroing (a shared pv).
+// taken[] must be all zero on entry; found entries are left set (make_after clears them).
+constexpr int kSearchLanes = 16;
+
+void choice_without_replacement(MT19937& rng, const int64_t* live, double* pv, bool pv_mutable, const double* base,
+                                size_t n, int64_t size, std::vector<uint8_t>& taken, std::vector<int64_t>& found,
+                                std::vector<double>& work, std::vector<double>& xs, std::vector<uint32_t>& js) {
   found.clear();
+  if (size <= 0 || n == 0) return;
   found.reserve((size_t)size);
-  std::vector<double> xs, cdf;
+  if (work.size() < n) work.resize(n);
+  double* const wk = work.data();
+  size_t wfrom = base == wk ? 0 : n;
+  size_t dirty = n;  // the smallest position whose p changed since the cdf was computed
+  double last = base[n - 1];
   while ((int64_t)found.size() < size) {
-    const int64_t m = size - (int64_t)found.size();
-    xs.resize((size_t)m);
-    for (int64_t i = 0; i < m; ++i) xs[(size_t)i] = rng.next_double();
-    if (!found.empty()) {  // p[found] = 0: drop them from the live list
-      size_t w = 0;
-      for (size_t i = 0; i < live.size(); ++i)
-        if (!taken[(size_t)live[i]]) live[w++] = live[i];
-      live.resize(w);
+    const size_t m = (size_t)(size - (int64_t)found.size());
+    xs.resize(m);
+    js.resize(m);
+    for (size_t i = 0; i < m; ++i) xs[i] = rng.next_double();
+    if (dirty < n) {  // p[found] = 0: cumsum again from the first changed position
+      double s = dirty ? (dirty - 1 < wfrom ? base[dirty - 1] : wk[dirty - 1]) : 0.0;
+      if (pv_mutable) {
+        for (size_t i = dirty; i < n; ++i) {
+          s += pv[i];
+          wk[i] = s;
+        }
+      } else {
+        for (size_t i = dirty; i < n; ++i) {
+          s += taken[(size_t)live[i]] ? 0.0 : pv[i];
+          wk[i] = s;
+        }
+      }
+      wfrom = std::min(wfrom, dirty);
+      last = s;
+      dirty = n;
     }
-    cdf.resize(live.size());
-    double s = 0.0;
-    for (size_t i = 0; i < live.size(); ++i) {
-      s += prob(live[i]);
-      cdf[i] = s;
+    // upper_bound: the first j with x < cdf[j] / last. Branch-free halving keeps the answer in
+    // [lo, lo + len]; at len == 1 it is lo or lo + 1.
+    for (size_t i0 = 0; i0 < m; i0 += kSearchLanes) {
+      const int lanes = (int)std::min<size_t>(kSearchLanes, m - i0);
+      size_t lo[kSearchLanes];
+      double x[kSearchLanes];
+      for (int g = 0; g < lanes; ++g) {
+        lo[g] = 0;
+        x[g] = xs[i0 + (size_t)g];
+      }
+      for (size_t len = n; len > 1;) {
+        const size_t half = len >> 1;
+        for (int g = 0; g < lanes; ++g) {
+          const size_t mid = lo[g] + half - 1;
+          const double c = mid < wfrom ? base[mid] : wk[mid];
+          lo[g] = (x[g] < c / last) ? lo[g] : lo[g] + half;
+        }
+        len -= half;
+      }
+      for (int g = 0; g < lanes; ++g) {
+        const double c = lo[g] < wfrom ? base[lo[g]] : wk[lo[g]];
+        size_t j = (x[g] < c / last) ? lo[g] : lo[g] + 1;
+        js[i0 + (size_t)g] = (uint32_t)(j < n ? j : n - 1);  // j == n cannot happen for x < 1; guard
+      }
     }
-    const double last = s;
-    for (size_t i = 0; i < cdf.size(); ++i) cdf[i] /= last;
-    for (int64_t i = 0; i < m; ++i) {
-      const size_t j = (size_t)(std::upper_bound(cdf.begin(), cdf.end(), xs[(size_t)i]) - cdf.begin());
-      // j == live.size() cannot happen for x < 1 = cdf.back(); guard anyway.
-      const int64_t v = live[j < live.size() ? j : live.size() - 1];
+    for (size_t i = 0; i < m; ++i) {  // first-occurrence order
+      const size_t j = js[i];
+      const int64_t v = live[j];
       if (!taken[(size_t)v]) {
         taken[(size_t)v] = 1;
         found.push_back(v);
+        if (pv_mutable) pv[j] = 0.0;
+        dirty = std::min(dirty, j);
       }
     }
   }
@@ -138,24 +188,37 @@ struct Graph {
 class Work {
  public:
   explicit Work(const Graph& g) : g_(g), cnt(g.N, 0), bits((g.N + 63) / 64), wrank((g.N + 63) / 64),
-                                  taken(g.N, 0), in_prev(g.N, 0) {}
+                                  taken(g.N, 0), in_prev(g.N, 0), counted(g.N, 0) {}
 
-  // This thread's Work for graph g, in the state of a freshly constructed one.
+  // This thread's Work for graph g, in the state of a freshly constructed one. A call that
+  // finished (finish()) left taken / in_prev clear and recorded what it set in cnt (live) and
+  // counted (counted_list): only those entries are reset — N-wide fills cost ~3 ms a batch on a
+  // 2.4 M-node graph. After a call that failed part-way everything is refilled.
   static Work& acquire(const Graph& g) {
     static thread_local std::unique_ptr<Work> tw;
     if (!tw || tw->g_.N != g.N) {
       tw.reset(new Work(g));
     } else {
       tw->g_ = g;
-      std::fill(tw->cnt.begin(), tw->cnt.end(), 0);
-      std::fill(tw->taken.begin(), tw->taken.end(), 0);
-      std::fill(tw->in_prev.begin(), tw->in_prev.end(), 0);
-      tw->counted.clear();
+      if (!tw->clean_) {
+        std::fill(tw->cnt.begin(), tw->cnt.end(), 0);
+        std::fill(tw->taken.begin(), tw->taken.end(), 0);
+        std::fill(tw->in_prev.begin(), tw->in_prev.end(), 0);
+        std::fill(tw->counted.begin(), tw->counted.end(), 0);
+      } else {
+        tw->reset_counts();
+        for (int64_t v : tw->counted_list) tw->counted[(size_t)v] = 0;
+      }
+      tw->counted_list.clear();
       tw->live.clear();
       tw->found.clear();
     }
+    tw->clean_ = false;
     return *tw;
   }
+
+  // The call ends with taken / in_prev clear (every successful sampler path restores them).
+  void finish() { clean_ = true; }
 
   // Row pointers of U = lap[rows, :] into fullrowptr; returns nnz(U) or -1 if >= 2^31.
   int64_t row_pointers(const std::vector<int64_t>& rows, std::vector<int32_t>& fullrowptr) const {
@@ -182,44 +245,119 @@ class Work {
   // counted yet are added; the counts are kept across layers (the layer-2 U has 5.7 M
   // entries of which 3.5 M are the layer-1 rows').
   int64_t count_columns_nested(const std::vector<int64_t>& rows) {
-    if (counted.empty()) counted.assign(g_.N, 0);
     for (int64_t v : rows) {
       if (!counted[(size_t)v]) {
         counted[(size_t)v] = 1;
+        counted_list.push_back(v);
         add_row(v);
       }
     }
     return scan_counts();
   }
 
+  // cnt[c] += entries of row v in column c (one random increment per entry: the sampler's
+  // costliest loop on large graphs — nothing else is done per entry)
   void add_row(int64_t v) {
     const int64_t b = g_.indptr[v], e = g_.indptr[v + 1];
     if (g_.data) {
-      for (int64_t k = b; k < e; ++k) cnt[(size_t)g_.indices[k]] += (g_.data[k] != 0.0f);
+      for (int64_t k = b; k < e; ++k) cnt[(uint32_t)g_.indices[k]] += (g_.data[k] != 0.0f);
     } else {
-      for (int64_t k = b; k < e; ++k) ++cnt[(size_t)g_.indices[k]];
+      for (int64_t k = b; k < e; ++k) ++cnt[(uint32_t)g_.indices[k]];
     }
   }
 
+  // live = the columns with a non-zero count, ascending; returns their sum. 16 counts per
+  // step compared at once; only the non-zero ones are visited (no per-column branch).
   int64_t scan_counts() {
     int64_t isum = 0;
     live.clear();
-    for (size_t c = 0; c < g_.N; ++c) {
-      if (cnt[c]) {
-        isum += cnt[c];
+    const int32_t* const c32 = cnt.data();
+    const size_t N = g_.N, N16 = N & ~(size_t)15;
+    const __m128i z = _mm_setzero_si128();
+    auto visit = [&](size_t c0, uint32_t mask) {
+      for (; mask; mask &= mask - 1) {
+        const size_t c = c0 + (size_t)__builtin_ctz(mask);
+        isum += c32[c];
         live.push_back((int64_t)c);
       }
+    };
+    for (size_t c0 = 0; c0 < N16; c0 += 16) {
+      const __m128i* q = reinterpret_cast<const __m128i*>(c32 + c0);
+      const uint32_t zm = (uint32_t)_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(_mm_loadu_si128(q), z))) |
+                          (uint32_t)_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(_mm_loadu_si128(q + 1), z))) << 4 |
+                          (uint32_t)_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(_mm_loadu_si128(q + 2), z))) << 8 |
+                          (uint32_t)_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(_mm_loadu_si128(q + 3), z))) << 12;
+      if (zm != 0xFFFFu) visit(c0, ~zm & 0xFFFFu);
     }
+    uint32_t tail = 0;
+    for (size_t c = N16; c < N; ++c) tail |= (uint32_t)(c32[c] != 0) << (c - N16);
+    visit(N16, tail);
     return isum;
   }
 
-  // p[v] = pi[v] / sum(pi) for the column counts (sampler.py:122)
-  auto count_prob(double total) const {
-    return [this, total](int64_t v) { return (double)cnt[(size_t)v] / total; };
+  // every non-zero count is in live (the last scan saw them all: counts only grow between scans,
+  // and clear_counts empties them)
+  void reset_counts() {
+    for (int64_t c : live) cnt[(size_t)c] = 0;
   }
+
+  // LADIES: choice over live with p[v] = pi[v] / sum(pi), the column counts (sampler.py:122);
+  // p and its cumsum in one pass (the divide and the add chain overlap)
+  void choose_by_counts(MT19937& rng, double total, int64_t s_num) {
+    const size_t n = live.size();
+    pv.resize(n);
+    if (cdf_work.size() < n) cdf_work.resize(n);
+    double s = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      const double q = (double)cnt[(size_t)live[i]] / total;
+      pv[i] = q;
+      s += q;
+      cdf_work[i] = s;
+    }
+    choice_without_replacement(rng, live.data(), pv.data(), true, cdf_work.data(), n, s_num, taken, found, cdf_work,
+                               xs, js);
+  }
+
+  // FastGCN: choice over the nodes with p > 0 (NaN p never live), layer-independent: the
+  // candidate list, their p and the untouched cdf are kept per thread for the p array they
+  // came from (identified by its address, length and 64 sampled values).
+  void choose_by_p(MT19937& rng, const double* p, int64_t s_num) {
+    const size_t N = g_.N;
+    uint64_t sig = 1469598103934665603ull;
+    for (size_t k = 0; k < 64; ++k) {
+      uint64_t b;
+      std::memcpy(&b, &p[(k * (N - 1)) / 63], 8);
+      sig = (sig ^ b) * 1099511628211ull;
+    }
+    if (fg_p != p || fg_n != N || fg_sig != sig) {
+      fg_live.clear();
+      fg_pv.clear();
+      for (size_t v = 0; v < N; ++v) {
+        if (p[v] > 0.0) {
+          fg_live.push_back((int64_t)v);
+          fg_pv.push_back(p[v]);
+        }
+      }
+      fg_base.resize(fg_pv.size());
+      double s = 0.0;
+      for (size_t i = 0; i < fg_pv.size(); ++i) {
+        s += fg_pv[i];
+        fg_base[i] = s;
+      }
+      fg_p = p;
+      fg_n = N;
+      fg_sig = sig;
+    }
+    choice_without_replacement(rng, fg_live.data(), fg_pv.data(), false, fg_base.data(), fg_live.size(),
+                               std::min<int64_t>((int64_t)fg_live.size(), s_num), taken, found, cdf_work, xs, js);
+  }
+
+  size_t fastgcn_candidates() const { return fg_live.size(); }
 
   void clear_counts() {
     for (int64_t c : live) cnt[(size_t)c] = 0;
+    for (int64_t v : counted_list) counted[(size_t)v] = 0;
+    counted_list.clear();
   }
 
   // after = unique(concat(found, prev)), ascending; then the membership bitmap of `after`
@@ -336,7 +474,15 @@ class Work {
   std::vector<uint64_t> bits;
   std::vector<int32_t> wrank;
   std::vector<uint8_t> taken, in_prev, counted;
-  std::vector<int64_t> live, found;
+  std::vector<int64_t> live, found, counted_list;
+  std::vector<double> pv, cdf_work, xs;  // choice scratch
+  std::vector<uint32_t> js;
+  std::vector<int64_t> fg_live;          // FastGCN candidates (see choose_by_p)
+  std::vector<double> fg_pv, fg_base;
+  const double* fg_p = nullptr;
+  size_t fg_n = 0;
+  uint64_t fg_sig = 0;
+  bool clean_ = true;
 };
 
 int check_inputs(const char* who, const int64_t* indptr, const int32_t* indices, int64_t num_nodes,
@@ -433,7 +579,7 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       const double total = (double)isum;
       const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[d]);
       L.s_num = s_num;
-      choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
+      w.choose_by_counts(rng, total, s_num);
       w.make_after(prev, after, !dev);
       if (dev) {
         if (!w.device_layer(prev, after, indptr_t, L) || L.nnz >= ((int64_t)1 << 31))
@@ -448,12 +594,12 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       if (!nested) {
         w.clear_counts();
         nested = true;  // after = unique(...): from here on every layer's rows are unique
-        w.counted.clear();
       }
       prev.swap(after);  // after ⊇ prev: the next layer's counts extend these
     }
     res->input_nodes = prev;
     *out = res.release();
+    w.finish();
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_ladies_sample: out of host memory");
@@ -483,7 +629,7 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
     if (isum == 0) return fail("gnn_subgraph_sample: probabilities contain NaN (no entries in U)");
     const double total = (double)isum;
     const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[0]);
-    choice_without_replacement(rng, w.count_prob(total), w.live, s_num, w.taken, w.found);
+    w.choose_by_counts(rng, total, s_num);
     w.make_after(batch, after);
     // ... the top-most layer with a non-zero order takes U[:, after] (sampler.py:42-53) ...
     int32_t d = 0;
@@ -517,6 +663,7 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
     }
     res->input_nodes = after;
     *out = res.release();
+    w.finish();
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_subgraph_sample: out of host memory");
@@ -537,10 +684,6 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
     std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
     res->layers.resize((size_t)num_layers);
     MT19937 rng(seed);
-    // the layer-independent importance: live = ascending nodes with p > 0 (NaN p never live)
-    std::vector<int64_t> live;
-    for (int64_t v = 0; v < num_nodes; ++v)
-      if (p[v] > 0.0) live.push_back(v);
     std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size), after;
     for (int32_t d = 0; d < num_layers; ++d) {
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];
@@ -548,9 +691,10 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
       L.present = true;
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
       if (unnz < 0) return fail("gnn_fastgcn_sample: sub-graph nnz >= 2^31");
-      const int64_t s_num = std::min<int64_t>((int64_t)live.size(), samp_num[d]);
+      // the layer-independent importance: candidates = ascending nodes with p > 0
+      w.choose_by_p(rng, p, samp_num[d]);
+      const int64_t s_num = std::min<int64_t>((int64_t)w.fastgcn_candidates(), samp_num[d]);
       L.s_num = s_num;
-      choice_without_replacement(rng, [p](int64_t v) { return p[v]; }, live, s_num, w.taken, w.found);
       // after = unique(sampled): layers are sampled independently (no union with prev)
       after.assign(w.found.begin(), w.found.end());
       std::sort(after.begin(), after.end());
@@ -565,6 +709,7 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
     }
     res->input_nodes = prev;
     *out = res.release();
+    w.finish();
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_fastgcn_sample: out of host memory");

@@ -158,6 +158,20 @@ def test_native_threads_match_sequential():
         _same(a, b)
 
 
+def test_native_scratch_reuse_across_graphs_and_kinds():
+    """The per-thread scratch is reset from what the previous call touched (not refilled), and
+    FastGCN's candidate list / base cdf is cached per p array: alternating two graphs of the
+    same size and all three samplers on one thread must still match numpy call for call."""
+    N = 4000
+    laps = [_lap(N, 15, 31), _lap(N, 9, 32, sigma=0.5)]
+    for it in range(3):
+        for gi, lap in enumerate(laps):
+            for kind in ("ladies", "fastgcn", "subgraph"):
+                batch = np.random.default_rng(10 * it + gi).permutation(N)[:150]
+                a, b = _both(lap, N, batch, [900] * 3, [1, 1, 1], 100 * it + gi, kind=kind)
+                _same(a, b)
+
+
 def test_native_isolated_batch_raises_like_numpy():
     """A layer whose rows have no entries: p = 0/0 and numpy's choice raises; so does native."""
     N = 50
