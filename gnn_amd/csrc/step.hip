@@ -267,10 +267,23 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     return f;
   }();
   const int training = (int)d[GNN_SH_TRAINING];
+  // optional per-aggregation timing (GNN_SH_TIMING): arm the caller's event pair for the next
+  // SpMM launch (gnn_spmm_set_timing_events) and record the call's shape beside it
+  int64_t* const T = HP<int64_t>(d, GNN_SH_TIMING);
+  int64_t nrec = 0;
+  auto arm = [&](int64_t kind, int64_t l, int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t Fk, int64_t ldx,
+                 int64_t ldo, const void* X, const void* Y, int64_t res_rows) {
+    if (!T || nrec >= T[0]) return;
+    int64_t* r = T + 1 + GNN_STEP_TIMING_SLOTS * nrec++;
+    gnn_spmm_set_timing_events((void*)r[0], (void*)r[1]);
+    const int64_t v[] = {kind, l, M, K, nnz, F, Fk, ldx, ldo, (int64_t)(uintptr_t)X, (int64_t)(uintptr_t)Y, res_rows, 1};
+    std::memcpy(r + 2, v, sizeof v);
+  };
   // ------------------------------------------------------------------ forward
   for (int l = 0; l < pl.nl; ++l) {
     LayerBufs& b = pl.lb[l];
     const int64_t N = b.N;
+    arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
     GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
                              P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
                              b.ws_fwd, b.b_fwd, 0, st));
@@ -357,10 +370,12 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_TROWPTR) != nullptr, "gnn_train_step: layer %d has no transpose", l);
       if (pl.sage) {
         GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_RMAP) != nullptr, "gnn_train_step: layer %d has no row map", l);
+        arm(1, l, b.K, b.M, b.nnz, b.F, b.F, b.F, b.F, b.dfeat, prev.dY, b.M);
         GNN_TRY(gnn_spmm_csr_f32_ex(P<const int32_t>(d, l, GNN_SL_TROWPTR), P<const int32_t>(d, l, GNN_SL_TCOL),
                                     P<const float>(d, l, GNN_SL_TVAL), b.K, b.M, b.nnz, b.dfeat, b.F, prev.dY, b.F,
                                     b.F, b.dxs, b.F, P<const int32_t>(d, l, GNN_SL_RMAP), b.ws_bwd, b.b_bwd, 0, st));
       } else {
+        arm(1, l, b.K, b.M, b.nnz, b.F, b.F, b.F, b.F, b.dfeat, prev.dY, 0);
         GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_TROWPTR), P<const int32_t>(d, l, GNN_SL_TCOL),
                                  P<const float>(d, l, GNN_SL_TVAL), b.K, b.M, b.nnz, b.dfeat, b.F, prev.dY, b.F, b.F,
                                  b.ws_bwd, b.b_bwd, 0, st));

@@ -72,6 +72,25 @@ def take_timing_records(sync: bool = True):
     return out
 
 
+def timing_enabled() -> bool:
+    return _timing_enabled
+
+
+def record_timing(tag, e0, e1, M, K, nnz, F, Fk, ldx, ldy, xptr, yptr, unit_nnz, res_rows, residual) -> None:
+    """Append one timed aggregation launch (events e0 / e1 armed around its main kernel) — also
+    used by the native step executor, whose launches are armed from C (gnn_amd.executor)."""
+    L = _lib.lib()
+    cfg = (ctypes.c_int32 * 6)()
+    L.gnn_spmm_config(M, K, nnz, Fk, ldx, ldy, xptr, yptr, unit_nnz, cfg)
+    u = 4 if cfg[2] <= 4 else (3 if cfg[2] == 5 else 2)  # pick_u (spmm.hip)
+    nbytes = algorithmic_bytes(M, nnz, F)
+    if residual:  # residual rows read + the row map
+        nbytes += res_rows * F * 4 + M * 4
+    res = "true" if residual else "false"
+    _timing_records.append((tag, e0, e1, nbytes, f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>",
+                            dict(M=M, K=K, nnz=nnz, F=F, res_rows=res_rows if residual else 0)))
+
+
 def algorithmic_bytes(M: int, nnz: int, F: int) -> int:
     """gathered X rows + (col, val) + rowptr + Y write."""
     return nnz * F * 4 + nnz * 8 + (M + 1) * 4 + M * F * 4
@@ -239,17 +258,8 @@ def spmm_csr(op: CsrOperand, dense: torch.Tensor, tag: str = "fwd", unit_nnz: in
             e0.record()  # creates the underlying hipEvent; the library re-records it
             e1.record()
             L.gnn_spmm_set_timing_events(e0.cuda_event, e1.cuda_event)
-            cfg = (ctypes.c_int32 * 6)()
-            L.gnn_spmm_config(M, K, op.nnz, Fk, ldx, ldo, dense.data_ptr(), out.data_ptr(), unit_nnz, cfg)
-            u = 4 if cfg[2] <= 4 else (3 if cfg[2] == 5 else 2)  # pick_u (spmm.hip)
-            nbytes = algorithmic_bytes(M, op.nnz, F)
-            if rmap is not None:  # residual rows read + the row map
-                nbytes += residual.shape[0] * F * 4 + M * 4
-            res = "true" if rmap is not None else "false"
-            _timing_records.append((tag, e0, e1, nbytes,
-                                    f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>",
-                                    dict(M=M, K=K, nnz=op.nnz, F=F,
-                                         res_rows=residual.shape[0] if rmap is not None else 0)))
+            record_timing(tag, e0, e1, M, K, op.nnz, F, Fk, ldx, ldo, dense.data_ptr(), out.data_ptr(), unit_nnz,
+                          residual.shape[0] if rmap is not None else 0, rmap is not None)
         if rmap is None:
             _lib.check(L.gnn_spmm_csr_f32(_ptr(op.rowptr), _ptr(op.col), _ptr(op.val), M, K, op.nnz,
                                           dense.data_ptr(), ldx, out.data_ptr(), ldo, Fk,

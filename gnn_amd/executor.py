@@ -20,10 +20,12 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import custom_sparse_ops as cso
 
 VERSION, MAX_LAYERS, HEADER, LAYER_SLOTS, SAGE, GCN = 1, 4, 24, 32, 0, 1
 (H_VERSION, H_LAYERS, H_KIND, H_X0, H_LDX0, H_F0, H_HEAD_W, H_HEAD_B, H_HEAD_GW, H_HEAD_GB, H_CLASSES, H_LABELS,
- H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID) = range(18)
+ H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING) = range(19)
+TIMING_SLOTS = 16
 (L_ROWPTR, L_COL, L_VAL, L_M, L_K, L_NNZ, L_TROWPTR, L_TCOL, L_TVAL, L_SAMPLED, L_NSAMPLED, L_RMAP, L_WW, L_BW,
  L_WB, L_BB, L_SCALE, L_OFFSET, L_GWW, L_GBW, L_GWB, L_GBB, L_GSCALE, L_GOFFSET, L_SEED) = range(25)
 
@@ -147,6 +149,7 @@ class NativeStep:
         d[H_HEAD_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if tr else 0
         loss = torch.empty((), dtype=torch.float32, device=x0.device)
         d[H_LOSS] = loss.data_ptr()
+        timing = self._arm_timing(d, len(adjs)) if cso.timing_enabled() else None
         L = _lib.lib()
         dp = d.ctypes.data
         wsb = L.gnn_train_step_workspace_bytes(dp)
@@ -155,6 +158,35 @@ class NativeStep:
         ws = torch.empty(wsb, dtype=torch.uint8, device=x0.device)
         with _lib.on_device(x0.device):
             _lib.check(L.gnn_train_step_f32(dp, ws.data_ptr(), wsb, _lib.stream_of(x0.device)), "gnn_train_step_f32")
+        if timing is not None:
+            self._collect_timing(*timing)
         for p, gr in zip(self.params, self.grads):
             p.grad = gr
         return loss
+
+    @staticmethod
+    def _arm_timing(d, nl):
+        """custom_sparse_ops timing is on (bench roofline): one event pair per aggregation launch
+        (nl forwards + nl - 1 backwards), armed by the executor around its SpMM kernels."""
+        n = 2 * nl - 1
+        T = np.zeros(1 + TIMING_SLOTS * n, dtype=np.int64)
+        T[0] = n
+        evs = []
+        for i in range(n):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()  # creates the underlying hipEvent; the library re-records it
+            e1.record()
+            T[1 + TIMING_SLOTS * i], T[2 + TIMING_SLOTS * i] = e0.cuda_event, e1.cuda_event
+            evs.append((e0, e1))
+        d[H_TIMING] = T.ctypes.data
+        return T, evs
+
+    @staticmethod
+    def _collect_timing(T, evs):
+        for i, (e0, e1) in enumerate(evs):
+            r = T[1 + TIMING_SLOTS * i: 1 + TIMING_SLOTS * (i + 1)]
+            if r[14] != 1:
+                continue
+            kind, l, M, K, nnz, F, Fk, ldx, ldy, xp, yp, res = (int(v) for v in r[2:14])
+            cso.record_timing("fwd" if kind == 0 else "bwd", e0, e1, M, K, nnz, F, Fk, ldx, ldy, xp, yp, 0, res,
+                              kind == 1 and res > 0)

@@ -91,3 +91,27 @@ def test_executor_rejects_foreign_operands(dev):
     tb = _trainer(model_name, F, ncls, dev, native=True)
     coo = db.adjs[0].to_torch_coo()
     assert not tb.executor.supports(x0, [coo] + list(db.adjs[1:]), db.sampled_nodes, db.labels)
+
+
+def test_executor_timing_records_match_python_path(dev):
+    """bench.py's roofline times the aggregation launches with HIP events: through the executor
+    (armed from C, GNN_SH_TIMING) the records carry the same call sites, kernel names, shapes and
+    byte counts as through the autograd path."""
+    from gnn_amd import custom_sparse_ops as cso
+
+    model_name, F, ncls, db, x0 = _batch("reddit_sage", dev)
+    out = []
+    for native in (False, True):
+        tr = _trainer(model_name, F, ncls, dev, native=native)
+        cso.take_timing_records()
+        cso.enable_timing(True)
+        try:
+            tr.step(x0, db.adjs, db.sampled_nodes, db.labels)
+        finally:
+            cso.enable_timing(False)
+        out.append(cso.take_timing_records())
+    py, nat = out
+    assert len(py) == len(nat) == 5
+    for a, b in zip(py, nat):
+        assert a[0] == b[0] and a[2] == b[2] and a[3] == b[3] and a[4] == b[4], (a, b)
+        assert b[1] > 0
