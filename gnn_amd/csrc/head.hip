@@ -5,8 +5,8 @@
 // BCEWithLogitsLoss(weight = 1/batch per row, reduction = "sum"). In torch that is ~12
 // launches forward and ~14 backward for a 512 x 1024 input. Here four waves share a row: the
 // row norm by shuffles + LDS, the inverted-dropout mask from a counter hash (regenerated in the
-// backward, nothing stored), the C <= 64 logits as wave dot products against W (L2-resident,
-// 168 KB), and the per-row loss; a one-workgroup launch adds the rows in a fixed order. The
+// backward, nothing stored), the C <= 256 logits as wave dot products against W (L2-resident:
+// 168 KB for 41 classes x 1024, 704 KB for ogbn-papers' 172), and the per-row loss; a one-workgroup launch adds the rows in a fixed order. The
 // backward recomputes the normalised row, forms dz = w (sigmoid(z) - y), back-projects it
 // through W and the normalisation; dW = dzᵀ·xd and db = Σ dz are a small GEMM + sum.
 #include <hip/hip_runtime.h>
@@ -23,7 +23,8 @@ using gnn::ceil_div;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int HEAD_MAXC = 64;   // classes
+constexpr int HEAD_MAXC = 256;  // classes: lane j holds classes j, j + 64, j + 128, j + 192
+constexpr int HEAD_CQ = HEAD_MAXC / 64;
 constexpr int HEAD_MAXV = 8;    // 4-float pieces per lane: D <= 64 * 4 * 8 = 2048
 
 __device__ __forceinline__ float wave_sum(float x) {
@@ -149,14 +150,18 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float* __restrict__
   }
   __syncthreads();
   if (w != 0) return;
-  // lane j: logit j and its BCE term
+  // lane j: logits j, j + 64, ... and their BCE terms
   float term = 0.0f;
-  if (lane < C) {
-    const float z = ((part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane])) + (bias ? bias[lane] : 0.0f);
-    Z[(int64_t)r * C + lane] = z;
-    const float y = Y[(int64_t)r * ldy_lab + lane];
-    // BCE with logits, stable form: max(z, 0) - z y + log1p(exp(-|z|))
-    term = fmaxf(z, 0.0f) - z * y + log1pf(expf(-fabsf(z)));
+#pragma unroll
+  for (int q = 0; q < HEAD_CQ; ++q) {
+    const int j = lane + 64 * q;
+    if (j < C) {
+      const float z = ((part[0][j] + part[1][j]) + (part[2][j] + part[3][j])) + (bias ? bias[j] : 0.0f);
+      Z[(int64_t)r * C + j] = z;
+      const float y = Y[(int64_t)r * ldy_lab + j];
+      // BCE with logits, stable form: max(z, 0) - z y + log1p(exp(-|z|))
+      term += fmaxf(z, 0.0f) - z * y + log1pf(expf(-fabsf(z)));
+    }
   }
   const float loss = wave_sum(term);
   if (lane == 0) {
@@ -190,13 +195,18 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
   const float inv_keep = 1.0f / (1.0f - p);
   const bool tr = training != 0 && p > 0.0f;
   const float g = gloss ? *gloss : 1.0f;
-  // dz_j = g * w * (sigmoid(z_j) - y_j), one class per lane (C <= 64), in every wave
-  float dz = 0.0f;
-  if (lane < C) {
-    const float z = Z[(int64_t)r * C + lane];
-    const float sg = 1.0f / (1.0f + expf(-z));
-    dz = g * row_weight * (sg - Y[(int64_t)r * ldy_lab + lane]);
-    if (w == 0) DZ[(int64_t)r * C + lane] = dz;
+  // dz_j = g * w * (sigmoid(z_j) - y_j), classes lane + 64 q per lane, in every wave
+  float dz[HEAD_CQ];
+#pragma unroll
+  for (int q = 0; q < HEAD_CQ; ++q) {
+    const int j = lane + 64 * q;
+    dz[q] = 0.0f;
+    if (j < C) {
+      const float z = Z[(int64_t)r * C + j];
+      const float sg = 1.0f / (1.0f + expf(-z));
+      dz[q] = g * row_weight * (sg - Y[(int64_t)r * ldy_lab + j]);
+      if (w == 0) DZ[(int64_t)r * C + j] = dz[q];
+    }
   }
   // this wave's pieces of dxd = Wᵀ dz, then through dropout and the normalisation
   f4 dxd[PV], xn[PV];
@@ -211,9 +221,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
 #pragma unroll
       for (int i = 0; i < PV; ++i) wc[u][i] = wn[u][i];
     if (j0 + CB < C) load_w_block<PV>(wn, W, j0 + CB, C, D, w, lane);
+    const int qb = j0 >> 6;  // a block of CB classes lies in one 64-class slot
+    const float dzq = qb == 0 ? dz[0] : qb == 1 ? dz[1] : qb == 2 ? dz[2] : dz[3];
 #pragma unroll
     for (int u = 0; u < CB; ++u) {
-      const float dzj = __shfl(dz, j0 + u);  // lanes >= C hold 0
+      const float dzj = __shfl(dzq, (j0 + u) & 63);  // classes >= C hold 0
 #pragma unroll
       for (int i = 0; i < PV; ++i) dxd[i] += dzj * wc[u][i];
     }

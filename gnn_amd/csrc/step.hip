@@ -189,7 +189,7 @@ int plan(const int64_t* d, Arena& ar, Plan& pl) {
   pl.Mh = top.M;
   pl.Dh = top.D;
   pl.C = d[GNN_SH_CLASSES];
-  GNN_REQUIRE(pl.C > 0 && pl.C <= 64 && pl.Dh % 4 == 0 && pl.Dh <= 2048, "gnn_train_step: head %lld x %lld",
+  GNN_REQUIRE(pl.C > 0 && pl.C <= 256 && pl.Dh % 4 == 0 && pl.Dh <= 2048, "gnn_train_step: head %lld x %lld",
               (long long)pl.Dh, (long long)pl.C);
   pl.xd = ar.take<float>(pl.Mh * pl.Dh);
   pl.z = ar.take<float>(pl.Mh * pl.C);

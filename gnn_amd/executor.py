@@ -109,7 +109,7 @@ class NativeStep:
                 and labels.dim() == 2 and labels.stride(1) == 1):
             return False
         C, D = self.model.linear.weight.shape
-        if C > 64 or D % 4 or D > 2048 or labels.shape[1] != C:  # the fused head's contract (fused.head_supported)
+        if C > 256 or D % 4 or D > 2048 or labels.shape[1] != C:  # the fused head's contract (fused.head_supported)
             return False
         for li, op in enumerate(adjs):
             if not isinstance(op, CsrOperand):

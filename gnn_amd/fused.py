@@ -407,7 +407,7 @@ def head_supported(x: torch.Tensor, W: torch.Tensor, labels: torch.Tensor) -> bo
     M, D = x.shape
     return (x.is_cuda and x.dtype == torch.float32 and W.dtype == torch.float32 and x.stride(1) == 1
             and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0 and D % 4 == 0 and D <= 2048
-            and W.shape[0] <= 64 and labels.shape == (M, W.shape[0]))
+            and W.shape[0] <= 256 and labels.shape == (M, W.shape[0]))
 
 
 def head_bce_loss(x: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor], labels: torch.Tensor,

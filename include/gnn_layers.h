@@ -79,7 +79,7 @@ int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_
  *   *loss = Σ_rows Σ_j (max(z,0) - z y + log1p(exp(-|z|))) / M   (rows summed in fixed order)
  * norm[M] = ||x|| per row, rowloss[M] = the per-row terms (workspace). W is C x D row-major
  * (nn.Linear.weight), labels M x C with row stride ldl; bias may be NULL. D % 4 == 0,
- * D <= 2048, C <= 64; X, W, xd 16-byte aligned. Dropout: the counter hash of (seed, r*D+c)
+ * D <= 2048, C <= 256; X, W, xd 16-byte aligned. Dropout: the counter hash of (seed, r*D+c)
  * (as gnn_sage_norm_*), training = 0 or p = 0 disables it.
  * Backward: dz = (*grad_loss) (sigmoid(z) - y) / M (M x C, written for dW / db), and
  * dX = d/dx of the normalisation applied to mask · (dz·W). grad_loss may be NULL (1).

@@ -27,6 +27,10 @@ def _batch(name, dev):
     if name == "reddit_sage":
         A, labels, feats, ncls, train, *_ = graphs.make_dataset(graphs.REDDIT, seed=0)
         lap, model, samp, bs = graphs.lap_matrix(A, "graphsage"), "graphsage", 8192, 512
+    elif name == "tiny_sage_172":  # ogbn-papers' class count (the fused head up to 256 classes)
+        spec = graphs.GraphSpec("tiny172", 3000, 15000, 128, 172, 0.66, 0.1)
+        A, labels, feats, ncls, train, *_ = graphs.make_dataset(spec, seed=2)
+        lap, model, samp, bs = graphs.lap_matrix(A, "graphsage"), "graphsage", 600, 64
     else:
         A, labels, feats, ncls, train, *_ = graphs.make_dataset(graphs.TINY, seed=1)
         lap, model, samp, bs = graphs.lap_matrix(A, "gcn"), "gcn", 600, 64
@@ -60,7 +64,7 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
-@pytest.mark.parametrize("name", ["reddit_sage", "tiny_gcn"])
+@pytest.mark.parametrize("name", ["reddit_sage", "tiny_gcn", "tiny_sage_172"])
 def test_executor_matches_python_step(dev, name):
     model_name, F, ncls, db, x0 = _batch(name, dev)
     ta = _trainer(model_name, F, ncls, dev, native=False)

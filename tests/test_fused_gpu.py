@@ -149,7 +149,8 @@ def _head_ref(x, W, b, y, mask=None, p=0.0):
     return loss(z, y, True, x.device), z
 
 
-@pytest.mark.parametrize("M,D,C", [(512, 1024, 41), (37, 512, 41), (1, 64, 3), (100, 2048, 64), (5, 4, 1)])
+@pytest.mark.parametrize("M,D,C", [(512, 1024, 41), (37, 512, 41), (1, 64, 3), (100, 2048, 64), (5, 4, 1),
+                                   (512, 1024, 172), (33, 2048, 256), (7, 512, 65)])
 def test_head_bce_matches_torch(dev, M, D, C):
     """Fused head + BCE (gnn_head_bce_*), eval mode, against an fp64 torch evaluation:
     rtol 1e-4 / atol 1e-5 (row reductions of up to 2048 terms in another order)."""
