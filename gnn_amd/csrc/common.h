@@ -19,6 +19,12 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // out[0..n] = exclusive prefix of in[0..n) (out[n] = total), one workgroup (spmm.hip).
 int launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st);
 
+// gnn_gemm_f32_split3 with the split-k choice made for a batch of split_nbatch products
+// (gemm.hip): one product of a batch launched on its own, bit-identical to the batched result.
+int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, int split_nbatch,
+                         const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                         int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+
 }  // namespace gnn
 
 #define GNN_REQUIRE(cond, ...)                              \

@@ -564,9 +564,11 @@ enum Algo { ALGO_F32 = 0, ALGO_S3 = 1 };
 
 int64_t slots_of(int algo) { return algo == ALGO_S3 ? SLOTS_S3 : SLOTS_F32; }
 
+// split_nbatch: the batch count the split-k choice is made for (0: nbatch). A product launched
+// alone with split_nbatch = n sums in exactly the order it would inside a batch of n.
 int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
              int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
-             size_t workspace_bytes, void* stream) {
+             size_t workspace_bytes, void* stream, int split_nbatch = 0) {
   GNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gnn_gemm_f32: negative size");
   GNN_REQUIRE(M < INT_MAX && N < INT_MAX && K < INT_MAX, "gnn_gemm_f32: sizes must be < 2^31");
   GNN_REQUIRE(nbatch >= 1 && nbatch <= MAX_BATCH, "gnn_gemm_f32: nbatch must be 1..%d", MAX_BATCH);
@@ -591,7 +593,7 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   const int64_t bbytes = K == 0 ? 0 : ((b_kmajor ? K : N) - 1) * ldb * 4 + (b_kmajor ? N : K) * 4;
   if (algo == ALGO_S3 && (abytes >= INT_MAX || bbytes >= INT_MAX)) algo = ALGO_F32;
   hipStream_t st = (hipStream_t)stream;
-  const int splits = K == 0 ? 1 : pick_splits(M, N, K, nbatch, slots_of(algo));
+  const int splits = K == 0 ? 1 : pick_splits(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch, slots_of(algo));
   // XCD-aware tile map for split3 (2-8 % per layer pair, scripts/gemm_bench.py); GNN_GEMM_XCD=0 turns it off
   int xcdm = 1;
   if (const char* e = getenv("GNN_GEMM_XCD")) xcdm = atoi(e) != 0;
@@ -682,3 +684,14 @@ int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_
 }
 
 }  // extern "C"
+
+namespace gnn {
+
+int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, int split_nbatch,
+                         const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
+                         int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_run(ALGO_S3, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
+                  stream, split_nbatch);
+}
+
+}  // namespace gnn

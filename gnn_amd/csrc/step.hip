@@ -28,9 +28,12 @@
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 
 #include "common.h"
@@ -43,14 +46,20 @@ namespace {
 using gnn::align_up;
 using gnn::ceil_div;
 
-// db = Σ_rows dz (M x C, row-major): one thread per column, rows in order (deterministic).
+// db = Σ_rows dz (M x C, row-major): one workgroup per column, each thread a strided set of
+// rows, then a fixed-order tree (deterministic). A thread per column summing all M rows in a
+// dependent chain took ~48 us for 512 x 41.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ dz, int M, int C,
                                                      float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[4];
+  const int c = blockIdx.x;
   float s = 0.0f;
-  for (int r = 0; r < M; ++r) s += dz[(int64_t)r * C + c];
-  out[c] = s;
+  for (int r = threadIdx.x; r < M; r += 256) s += dz[(int64_t)r * C + c];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[c] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // A bump allocator over the workspace; with base == nullptr it only measures.
@@ -97,6 +106,59 @@ int blas_handle(rocblas_handle* h) {
   return 0;
 }
 
+// The aux stream of a (device, priority): the work of a layer that does not depend on its
+// aggregation — the x[sampled] gather and its GEMM in the forward, the weight-gradient GEMMs in
+// the backward — can run there, beside the L2-gather-bound SpMM on the caller's stream. Forked and joined with events from a small
+// per-stream pool; the pool's mutex is held for the whole step (events are re-recorded per call).
+struct Aux {
+  hipStream_t s = nullptr;
+  hipEvent_t ev[24] = {};
+  int next = 0;
+  std::mutex mu;
+  hipEvent_t take() { return ev[next++ % 24]; }
+};
+std::mutex g_aux_mu;
+Aux* g_aux[64][4] = {};
+
+int aux_of(hipStream_t st, Aux** out) {
+  int dev = 0;
+  GNN_HIP(hipGetDevice(&dev), "hipGetDevice");
+  GNN_REQUIRE(dev >= 0 && dev < 64, "gnn_train_step: device index %d", dev);
+  int prio = 0, lo = 0, hi = 0;
+  GNN_HIP(hipStreamGetPriority(st, &prio), "hipStreamGetPriority");
+  GNN_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+  const int slot = std::min(3, std::max(0, lo - prio));  // lo = least urgent
+  std::lock_guard<std::mutex> g(g_aux_mu);
+  Aux*& a = g_aux[dev][slot];
+  if (!a) {
+    std::unique_ptr<Aux> n(new Aux());
+    GNN_HIP(hipStreamCreateWithPriority(&n->s, hipStreamNonBlocking, prio), "hipStreamCreateWithPriority");
+    for (auto& e : n->ev) GNN_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags");
+    a = n.release();
+  }
+  *out = a;
+  return 0;
+}
+
+// `to` waits for everything issued so far on `from`
+int fork_join(Aux* a, hipStream_t from, hipStream_t to) {
+  hipEvent_t e = a->take();
+  GNN_HIP(hipEventRecord(e, from), "hipEventRecord");
+  GNN_HIP(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
+  return 0;
+}
+
+// GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
+// step it changed nothing (550 mini-batches/s either way; the layer-0/1 aggregations slowed from
+// 239 to 261 us while the GEMMs ran beside them — the CUs are already saturated).
+bool overlap_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("GNN_STEP_OVERLAP");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 // Row-major products on rocBLAS (column-major underneath): the small layer-2 / head products.
 int sgemm(rocblas_handle h, rocblas_operation ta, rocblas_operation tb, int64_t m, int64_t n, int64_t k,
           const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc) {
@@ -128,7 +190,7 @@ struct LayerBufs {
   const float* X;
   float *feat, *xs, *hB, *hW, *Y, *mean, *rstd;
   float *dY, *dhB, *dhW, *dxs, *dfeat;
-  void *ws_fwd, *ws_bwd, *ws_norm, *ws_gemm_f, *ws_gemm_dx, *ws_gemm_dw;
+  void *ws_fwd, *ws_bwd, *ws_norm, *ws_gemm_f, *ws_gemm_f2, *ws_gemm_dx, *ws_gemm_dw;
   size_t b_fwd, b_bwd, b_norm, b_gemm_f, b_gemm_dx, b_gemm_dw;
 };
 
@@ -184,6 +246,7 @@ int plan(const int64_t* d, Arena& ar, Plan& pl) {
     b.ws_fwd = ar.take<char>((int64_t)b.b_fwd);
     b.b_gemm_f = gnn_gemm_f32_split3_workspace_bytes(b.M, N, b.F, n);
     b.ws_gemm_f = ar.take<char>((int64_t)b.b_gemm_f);
+    b.ws_gemm_f2 = pl.sage ? ar.take<char>((int64_t)b.b_gemm_f) : nullptr;  // the aux stream's product
   }
   const LayerBufs& top = pl.lb[pl.nl - 1];
   pl.Mh = top.M;
@@ -267,6 +330,11 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     return f;
   }();
   const int training = (int)d[GNN_SH_TRAINING];
+  Aux* aux = nullptr;
+  if (overlap_enabled()) GNN_TRY(aux_of(st, &aux));
+  std::unique_lock<std::mutex> aux_lock;
+  if (aux) aux_lock = std::unique_lock<std::mutex>(aux->mu);
+  bool aux_used = false;
   // optional per-aggregation timing (GNN_SH_TIMING): arm the caller's event pair for the next
   // SpMM launch (gnn_spmm_set_timing_events) and record the call's shape beside it
   int64_t* const T = HP<int64_t>(d, GNN_SH_TIMING);
@@ -283,20 +351,44 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
   for (int l = 0; l < pl.nl; ++l) {
     LayerBufs& b = pl.lb[l];
     const int64_t N = b.N;
-    arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
-    GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
-                             P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
-                             b.ws_fwd, b.b_fwd, 0, st));
     const float* WB = P<const float>(d, l, GNN_SL_WB);
     const float* WW = P<const float>(d, l, GNN_SL_WW);
-    if (pl.sage) {
+    if (pl.sage)
       GNN_REQUIRE(L(d, l, GNN_SL_NSAMPLED) == b.M, "gnn_train_step: layer %d sampled %lld != M %lld", l,
                   (long long)L(d, l, GNN_SL_NSAMPLED), (long long)b.M);
-      GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M, b.F,
-                                  st));
-    }
     const bool ok = gemm_ok(b.feat, b.ldo) && gemm_ok(WW, b.F) && (!pl.sage || gemm_ok(WB, b.F));
-    if (ok && fills(b.M, N, n)) {
+    if (aux && pl.sage && ok && fills(b.M, N, n)) {
+      // x[sampled] and linearB on the aux stream beside A·X and linearW; each product launched
+      // alone with the split choice of the pair, so the sums are those of the batched launch
+      GNN_TRY(fork_join(aux, st, aux->s));
+      GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M, b.F,
+                                  aux->s));
+      const float* Ab[1] = {b.xs};
+      const float* Bb[1] = {WB};
+      float* Cb[1] = {b.hB};
+      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, Ab, b.ldo, Bb, b.F, Cb, N, b.ws_gemm_f2, b.b_gemm_f,
+                                        aux->s));
+      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                               b.ws_fwd, b.b_fwd, 0, st));
+      const float* Aw[1] = {b.feat};
+      const float* Bw[1] = {WW};
+      float* Cw[1] = {b.hW};
+      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, Aw, b.ldo, Bw, b.F, Cw, N, b.ws_gemm_f, b.b_gemm_f, st));
+      GNN_TRY(fork_join(aux, aux->s, st));
+    } else {
+      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                               b.ws_fwd, b.b_fwd, 0, st));
+      if (pl.sage)
+        GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M,
+                                    b.F, st));
+    }
+    if (aux && pl.sage && ok && fills(b.M, N, n)) {
+      // done above
+    } else if (ok && fills(b.M, N, n)) {
       const float* A[2] = {pl.sage ? b.xs : b.feat, b.feat};
       const float* B[2] = {pl.sage ? WB : WW, WW};
       float* Cc[2] = {pl.sage ? b.hB : b.hW, b.hW};
@@ -324,8 +416,8 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
                                pl.nrm, pl.dz, pl.dXh, pl.Dh, st));
   GNN_TRY(mm_gtx(h, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
   if (HP<float>(d, GNN_SH_HEAD_GB)) {
-    colsum_kernel<<<dim3((unsigned)ceil_div(pl.C, 256)), dim3(256), 0, st>>>(pl.dz, (int)pl.Mh, (int)pl.C,
-                                                                           HP<float>(d, GNN_SH_HEAD_GB));
+    colsum_kernel<<<dim3((unsigned)pl.C), dim3(256), 0, st>>>(pl.dz, (int)pl.Mh, (int)pl.C,
+                                                            HP<float>(d, GNN_SH_HEAD_GB));
     GNN_LAUNCHED("colsum_kernel");
   }
   for (int l = pl.nl - 1; l >= 0; --l) {
@@ -353,14 +445,21 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
         GNN_TRY(mm_gw(h, b.dhW, N, WW, b.F, b.dfeat, b.F, b.M, b.F, N));
       }
     }
-    // weight gradients: split over the sampled rows on split3 from 2048 rows, else rocBLAS
+    // weight gradients: split over the sampled rows on split3 from 2048 rows, else rocBLAS; on
+    // the aux stream (joined at the end of the step) beside the input-gradient GEMM + A_lᵀ·dfeat
     float* gWB = pl.sage ? P<float>(d, l, GNN_SL_GWB) : nullptr;
     float* gWW = P<float>(d, l, GNN_SL_GWW);
     if (ok && b.M >= 2048) {
       const float* X[2] = {pl.sage ? b.xs : b.feat, b.feat};
       float* Cc[2] = {pl.sage ? gWB : gWW, gWW};
+      hipStream_t sw = st;
+      if (aux && l >= 1) {
+        GNN_TRY(fork_join(aux, st, aux->s));
+        sw = aux->s;
+        aux_used = true;
+      }
       GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
-                                  b.b_gemm_dw, st));
+                                  b.b_gemm_dw, sw));
     } else {
       if (pl.sage) GNN_TRY(mm_gtx(h, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
       GNN_TRY(mm_gtx(h, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
@@ -382,6 +481,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       }
     }
   }
+  if (aux_used) GNN_TRY(fork_join(aux, aux->s, st));
   return 0;
 }
 
