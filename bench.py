@@ -94,6 +94,11 @@ def parse():
                     help="LADIES: bottom-up layers (below the top one) whose sub-graph the GPU extracts "
                          "(gnn_ladies_extract_f32) instead of the sampler threads: comma list, 'all' or 'none'")
     ap.add_argument("--host-extract", action="store_true", help="= --extract-layers none")
+    ap.add_argument("--column-counts", default="auto", choices=["auto", "host", "gpu"],
+                    help="LADIES draw: U's column counts summed by the sampler threads (host) or on the GPU "
+                         "(gnn_colcount_*, the graph resident in HBM); the draw itself stays on the host. auto: "
+                         "gpu from 1 M nodes (A/B on one box: ogbn-products-shaped 363 -> 720 mini-batches/s end "
+                         "to end; Reddit-shaped 558 host vs 516 gpu, where the host draw is not the bound)")
     ap.add_argument("--python-loader", action="store_true",
                     help="batch producer: Python worker threads calling the native sampler (BatchLoader) instead of "
                          "the C++ producer (NativeLoader: GIL-free workers, one blob and one H2D per batch)")
@@ -518,9 +523,13 @@ def main():
         dx = True
     else:
         dx = [int(v) for v in args.extract_layers.split(",") if v]
+    lkw = {}
+    counts_on_gpu = args.column_counts == "gpu" or (args.column_counts == "auto" and N >= 1_000_000)
+    if counts_on_gpu and args.sampler == "ladies" and not args.python_loader:
+        lkw["device_count"] = dev
     loader = (BatchLoader if args.python_loader else NativeLoader)(
         lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank, world_size=world,
-        store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx)
+        store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx, **lkw)
     if dx:  # the graph resident in HBM for the extraction (made once, outside every timed region)
         sampler.device_graph(loader.graph, dev)
         torch.cuda.synchronize()
@@ -571,12 +580,19 @@ def main():
             return pre[j].plan, lambda: (db.build_operands(), db)[1]
 
         pipeline(nxt_pre, nwarm)
-        cso.enable_timing(not args.no_roofline)
         stager.timing = []
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
-        cso.enable_timing(False)
-        recs = cso.take_timing_records()
         h_bytes, h_sec = stager.take_timing()
+        recs = []
+        if not args.no_roofline:
+            # the aggregation launches timed with HIP events in a second pass over the same
+            # batches (the per-launch events cost ~2-3 % of the step, so not in the timed pass)
+            k_[0] = nwarm
+            cso.enable_timing(True)
+            pipeline(nxt_pre, gsteps)
+            torch.cuda.synchronize()
+            cso.enable_timing(False)
+            recs = cso.take_timing_records()
         gpu_step = {"value": round(world * gsteps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / gsteps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / gsteps, 3),
@@ -659,7 +675,8 @@ def main():
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
                        "sampler_workers_per_rank": workers,
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
-                       "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host"},
+                       "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host",
+                       "column_counts": "gpu" if getattr(loader, "device_count", False) else "host"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,

@@ -69,6 +69,10 @@ _SIGNATURES = {
                                     ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _I64, _VP]),
     # include/gnn_extract.h
     "gnn_ladies_extract_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int32]),
+    "gnn_colcount_create": (_INT, [ctypes.c_int32, _I64, _VP, _VP, ctypes.POINTER(_VP)]),
+    "gnn_colcount_add": (_INT, [_VP, _VP, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_VP), ctypes.POINTER(_VP)]),
+    "gnn_colcount_reset": (_INT, [_VP]),
+    "gnn_colcount_destroy": (None, [_VP]),
     "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP,
                                       _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
     # include/gnn_step.h
@@ -103,11 +107,15 @@ _SAMPLER_SIGNATURES = {
     "gnn_ladies_input_nodes": (_INT, [_VP, _VP]),
     "gnn_ladies_free": (None, [_VP]),
     "gnn_mt19937_random_sample": (_INT, [ctypes.c_uint32, _I64, _VP]),
+    "gnn_sampler_profile": (_INT, [_VP, ctypes.c_int32, ctypes.c_int32]),
     "gnn_host_gather_rows_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _I64]),
     "gnn_loader_create": (_VP, [_VP, _VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32,
                                 _VP, _VP, _I64, _I64, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_int32, _VP,
                                 ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "gnn_loader_submit": (_INT, [_VP, ctypes.c_uint32, _VP, _I64]),
+    "gnn_loader_set_colcount": (_INT, [_VP, _VP]),
+    "gnn_ladies_sample_cc": (_INT, [_VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
+                                    ctypes.c_int32, _VP, _VP, ctypes.POINTER(_VP)]),
     "gnn_loader_next": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "gnn_batch_desc": (ctypes.POINTER(_I64), [_VP, ctypes.POINTER(_I64)]),
     "gnn_batch_blob": (_VP, [_VP]),

@@ -151,6 +151,7 @@ struct gnn_loader {
   std::vector<int32_t> orders;
   int32_t kind, device_extract, csc_from;
   const double* fastgcn_p;
+  gnn_colcount_api cc{};  // device column counting (cc.add == NULL: on the host)
   // machinery
   std::shared_ptr<Pool> pool;
   std::vector<std::thread> threads;
@@ -162,7 +163,7 @@ struct gnn_loader {
   bool stop = false;
 
   void run();
-  gnn_batch* produce(const Job& job);
+  gnn_batch* produce(const Job& job, void** cc_ctx);
 };
 
 namespace {
@@ -324,12 +325,21 @@ void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batc
 
 }  // namespace
 
-gnn_batch* gnn_loader::produce(const Job& job) {
+gnn_batch* gnn_loader::produce(const Job& job, void** cc_ctx) {
   std::unique_ptr<gnn_batch> b(new gnn_batch());
   b->id = job.id;
   gnn_ladies_result* res = nullptr;
   const int nl = (int)orders.size();
-  int rc;
+  int rc = 0;
+  const bool use_cc = cc.add != nullptr && kind == GNN_SAMPLER_LADIES;
+  if (use_cc && !*cc_ctx) {  // this worker's context, made on its first batch
+    rc = cc.create(cc.device, N, cc.indptr, cc.indices, cc_ctx);
+    if (rc != 0) {
+      b->rc = rc;
+      b->err = "gnn_loader: gnn_colcount_create failed";
+      return b.release();
+    }
+  }
   if (kind == GNN_SAMPLER_FASTGCN)
     rc = gnn_fastgcn_sample(indptr, indices, data, N, fastgcn_p, job.nodes.data(), (int64_t)job.nodes.size(),
                             samp.data(), orders.data(), nl, job.seed, &res);
@@ -337,8 +347,9 @@ gnn_batch* gnn_loader::produce(const Job& job) {
     rc = gnn_subgraph_sample(indptr, indices, data, N, job.nodes.data(), (int64_t)job.nodes.size(), samp.data(),
                              orders.data(), nl, job.seed, &res);
   else
-    rc = gnn_ladies_sample_dev(indptr, indices, data, indptr_t, N, job.nodes.data(), (int64_t)job.nodes.size(), samp.data(),
-                               orders.data(), nl, job.seed, device_extract, &res);
+    rc = gnn_ladies_sample_cc(indptr, indices, data, indptr_t, N, job.nodes.data(), (int64_t)job.nodes.size(),
+                              samp.data(), orders.data(), nl, job.seed, device_extract, use_cc ? &cc : nullptr,
+                              use_cc ? *cc_ctx : nullptr, &res);
   if (rc != 0) {
     b->rc = rc;
     b->err = gnn_sampler_last_error();
@@ -355,6 +366,14 @@ gnn_batch* gnn_loader::produce(const Job& job) {
 }
 
 void gnn_loader::run() {
+  void* cc_ctx = nullptr;
+  struct Close {
+    gnn_loader* ld;
+    void** ctx;
+    ~Close() {
+      if (*ctx && ld->cc.destroy) ld->cc.destroy(*ctx);
+    }
+  } close{this, &cc_ctx};
   for (;;) {
     Job job;
     {
@@ -364,7 +383,7 @@ void gnn_loader::run() {
       job = std::move(jobs.front());
       jobs.pop_front();
     }
-    gnn_batch* b = produce(job);
+    gnn_batch* b = produce(job, &cc_ctx);
     {
       std::lock_guard<std::mutex> lk(mu);
       done[b->id] = b;
@@ -424,6 +443,21 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
     gnn_smp::set_error(std::string("gnn_loader_create: ") + e.what());
     return nullptr;
   }
+}
+
+int gnn_loader_set_colcount(gnn_loader* ld, const gnn_colcount_api* api) {
+  if (!ld || !api || !api->create || !api->add || !api->reset || !api->destroy || !api->indptr || !api->indices
+      || ld->data) {
+    gnn_smp::set_error("gnn_loader_set_colcount: bad arguments (or a graph with stored zeros)");
+    return -22;
+  }
+  std::lock_guard<std::mutex> lk(ld->mu);
+  if (ld->next_id != 0) {
+    gnn_smp::set_error("gnn_loader_set_colcount: batches already submitted");
+    return -22;
+  }
+  ld->cc = *api;
+  return 0;
 }
 
 int gnn_loader_submit(gnn_loader* ld, uint32_t seed, const int64_t* nodes, int64_t n) {

@@ -9,7 +9,10 @@
 #include "sampler_internal.h"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <emmintrin.h>
@@ -23,6 +26,26 @@ using gnn_smp::Layer;
 namespace {
 
 thread_local std::string g_err;
+
+// Optional phase timers (GNN_SAMPLER_PROFILE=1): nanoseconds per phase summed over all threads,
+// read by gnn_sampler_profile (scripts/sampler_probe.py). One clock read per phase per layer.
+enum Phase { P_SCRATCH, P_ROWPTR, P_COUNT, P_DRAW, P_AFTER, P_EXTRACT, P_TAIL, P_CALLS, P_NPHASE };
+std::atomic<int64_t> g_prof[P_NPHASE];
+const bool g_prof_on = [] {
+  const char* e = getenv("GNN_SAMPLER_PROFILE");
+  return e && atoi(e) != 0;
+}();
+
+struct PhaseClock {
+  std::chrono::steady_clock::time_point t;
+  PhaseClock() : t(g_prof_on ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{}) {}
+  void lap(Phase p) {
+    if (!g_prof_on) return;
+    const auto n = std::chrono::steady_clock::now();
+    g_prof[p].fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count(), std::memory_order_relaxed);
+    t = n;
+  }
+};
 
 int fail(const char* fmt, ...) {
   char buf[512];
@@ -255,6 +278,51 @@ class Work {
     return scan_counts();
   }
 
+  // The same counts summed on the device (gnn_colcount_api): the rows not counted yet (nested)
+  // or all rows go to the GPU, live and cnt[live] come back. Returns the sum, or -1 (rc set).
+  int64_t count_columns_device(const std::vector<int64_t>& rows, bool nested, const gnn_colcount_api* cc, void* ctx,
+                               int* rc) {
+    const std::vector<int64_t>* send = &rows;
+    if (nested) {
+      newrows.clear();
+      for (int64_t v : rows) {
+        if (!counted[(size_t)v]) {
+          counted[(size_t)v] = 1;
+          counted_list.push_back(v);
+          newrows.push_back(v);
+        }
+      }
+      send = &newrows;
+    }
+    int64_t nlive = 0;
+    const uint64_t* bits = nullptr;
+    const int32_t* counts = nullptr;
+    *rc = cc->add(ctx, send->data(), (int64_t)send->size(), &nlive, &bits, &counts);
+    if (*rc) return -1;
+    live.clear();
+    live.reserve((size_t)nlive);
+    int64_t isum = 0, i = 0;
+    const size_t W = (g_.N + 63) / 64;
+    for (size_t wi = 0; wi < W; ++wi) {
+      for (uint64_t x = bits[wi]; x; x &= x - 1) {
+        const size_t c = (wi << 6) + (size_t)__builtin_ctzll(x);
+        if (i >= nlive || c >= g_.N) {
+          *rc = -5;
+          return -1;
+        }
+        cnt[c] = counts[i];
+        isum += counts[i];
+        live.push_back((int64_t)c);
+        ++i;
+      }
+    }
+    if (i != nlive) {
+      *rc = -5;
+      return -1;
+    }
+    return isum;
+  }
+
   // cnt[c] += entries of row v in column c (one random increment per entry: the sampler's
   // costliest loop on large graphs — nothing else is done per entry)
   void add_row(int64_t v) {
@@ -474,7 +542,7 @@ class Work {
   std::vector<uint64_t> bits;
   std::vector<int32_t> wrank;
   std::vector<uint8_t> taken, in_prev, counted;
-  std::vector<int64_t> live, found, counted_list;
+  std::vector<int64_t> live, found, counted_list, newrows;
   std::vector<double> pv, cdf_work, xs;  // choice scratch
   std::vector<uint32_t> js;
   std::vector<int64_t> fg_live;          // FastGCN candidates (see choose_by_p)
@@ -521,6 +589,15 @@ extern "C" {
 
 const char* gnn_sampler_last_error(void) { return g_err.c_str(); }
 
+int gnn_sampler_profile(double* out, int32_t n, int32_t reset) {
+  if (!out || n < 0) return fail("gnn_sampler_profile: bad arguments");
+  for (int32_t i = 0; i < n && i < P_NPHASE; ++i) {
+    const int64_t v = reset ? g_prof[i].exchange(0) : g_prof[i].load();
+    out[i] = i == P_CALLS ? (double)v : (double)v * 1e-9;
+  }
+  return g_prof_on ? 0 : 1;
+}
+
 int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out) {
   if (n < 0 || (n > 0 && !out)) return fail("gnn_mt19937_random_sample: bad arguments");
   MT19937 rng(seed);
@@ -540,19 +617,32 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
                           const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                           const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
                           gnn_ladies_result** out) {
+  return gnn_ladies_sample_cc(indptr, indices, data, indptr_t, num_nodes, batch_nodes, batch_size, samp_num, orders,
+                              num_layers, seed, device_extract, nullptr, nullptr, out);
+}
+
+int gnn_ladies_sample_cc(const int64_t* indptr, const int32_t* indices, const float* data, const int64_t* indptr_t,
+                         int64_t num_nodes, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                         const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
+                         const gnn_colcount_api* cc, void* cc_ctx, gnn_ladies_result** out) {
   if (int rc = check_inputs("gnn_ladies_sample", indptr, indices, num_nodes, batch_nodes, batch_size, samp_num,
                             orders, num_layers, out))
     return rc;
   if (device_extract && data)
     return fail("gnn_ladies_sample_dev: device extraction needs a graph without stored zeros (data == NULL)");
+  if (cc && (!cc_ctx || !cc->add || !cc->reset || data))
+    return fail("gnn_ladies_sample_cc: device counting needs a context and a graph without stored zeros");
   *out = nullptr;
   try {
     const Graph g{indptr, indices, data, (size_t)num_nodes};
+    PhaseClock clk;
     Work& w = Work::acquire(g);
     std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
     res->layers.resize((size_t)num_layers);
     MT19937 rng(seed);
     std::vector<int64_t> prev(batch_nodes, batch_nodes + batch_size), after;
+    clk.lap(P_SCRATCH);
+    if (g_prof_on) g_prof[P_CALLS].fetch_add(1, std::memory_order_relaxed);
     // A batch with repeated nodes repeats rows of U (counted twice); later layers' rows are
     // unique. Counts carry over between layers only when every layer's rows are unique.
     bool nested = true;
@@ -561,6 +651,9 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       w.in_prev[(size_t)v] = 1;
     }
     for (int64_t v : prev) w.in_prev[(size_t)v] = 0;
+    if (cc) {
+      if (int rc = cc->reset(cc_ctx)) return fail("gnn_ladies_sample: device column count reset failed (%d)", rc);
+    }
     bool top = true;  // the first sampled layer: its rows are the batch (any order, repeats)
     for (int32_t d = 0; d < num_layers; ++d) {
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];  // stored bottom-up
@@ -570,23 +663,32 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       // over the (bottom-up) layer index, -1 = every layer below the top one
       const bool dev = !top && ((device_extract >> (num_layers - 1 - d)) & 1);
       top = false;
+      clk.lap(P_TAIL);
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
       if (unnz < 0) return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
+      clk.lap(P_ROWPTR);
       // p = pi / sum(pi): exact integer sum
-      const int64_t isum = nested ? w.count_columns_nested(prev) : w.count_columns(prev);
+      int cc_rc = 0;
+      const int64_t isum = cc ? w.count_columns_device(prev, nested, cc, cc_ctx, &cc_rc)
+                              : (nested ? w.count_columns_nested(prev) : w.count_columns(prev));
+      if (cc_rc) return fail("gnn_ladies_sample: device column count failed (%d)", cc_rc);
+      clk.lap(P_COUNT);
       if (isum == 0)  // p = 0/0: numpy's choice raises "probabilities contain NaN"
         return fail("gnn_ladies_sample: probabilities contain NaN (layer %d: no entries in U)", d);
       const double total = (double)isum;
       const int64_t s_num = std::min<int64_t>((int64_t)w.live.size(), samp_num[d]);
       L.s_num = s_num;
       w.choose_by_counts(rng, total, s_num);
+      clk.lap(P_DRAW);
       w.make_after(prev, after, !dev);
+      clk.lap(P_AFTER);
       if (dev) {
         if (!w.device_layer(prev, after, indptr_t, L) || L.nnz >= ((int64_t)1 << 31))
           return fail("gnn_ladies_sample: sub-graph nnz >= 2^31");
       } else {
         w.extract(prev, unnz, L);
       }
+      clk.lap(P_EXTRACT);
       w.normfact(after, total, s_num, L);
       w.positions(after, prev, L);
       L.M = (int64_t)prev.size();
@@ -594,12 +696,16 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
       if (!nested) {
         w.clear_counts();
         nested = true;  // after = unique(...): from here on every layer's rows are unique
+        if (cc) {
+          if (int rc = cc->reset(cc_ctx)) return fail("gnn_ladies_sample: device column count reset failed (%d)", rc);
+        }
       }
       prev.swap(after);  // after ⊇ prev: the next layer's counts extend these
     }
     res->input_nodes = prev;
     *out = res.release();
     w.finish();
+    clk.lap(P_TAIL);
     return 0;
   } catch (const std::bad_alloc&) {
     return fail("gnn_ladies_sample: out of host memory");

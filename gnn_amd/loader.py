@@ -14,6 +14,7 @@ run is reproducible whatever the thread timing.
 from __future__ import annotations
 
 import collections
+import ctypes
 from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Iterator, Optional, Sequence
@@ -169,7 +170,6 @@ class NativeBatch:
     object dies — after the step that read it (the staging path keeps it alive until then)."""
 
     def __init__(self, handle: int, store: Optional[staging.FeatureStore]):
-        import ctypes
         import weakref
 
         from . import _lib
@@ -332,7 +332,9 @@ class NativeLoader:
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
                  seed: int = 0, devices=None, kind: str = "ladies", device_extract=False,
-                 pinned: Optional[bool] = None):
+                 pinned: Optional[bool] = None, device_count=None):
+        """device_count (LADIES, a graph without stored zeros): a torch device — the workers sum
+        U's column counts on it (gnn_colcount_*, the graph resident there) instead of on the host."""
         import scipy.sparse as sp
 
         from . import _lib
@@ -383,6 +385,11 @@ class NativeLoader:
             ptr(k["p"]), dx, 1, self.workers, int(bool(pinned)))
         if not self.handle:
             raise RuntimeError("gnn_loader_create failed: " + L.gnn_sampler_last_error().decode(errors="replace"))
+        self.device_count = device_count is not None and kind == "ladies" and g.data is None
+        if self.device_count:
+            self._keep["cc"] = smp.colcount_api(g, device_count)
+            _lib.check_sampler(L.gnn_loader_set_colcount(self.handle, ctypes.byref(self._keep["cc"])),
+                               "gnn_loader_set_colcount")
         self._pending = 0
 
     def _submit(self, nodes) -> None:
@@ -395,8 +402,6 @@ class NativeLoader:
         self._pending += 1
 
     def _next(self) -> LoadedBatch:
-        import ctypes
-
         from . import _lib
 
         h = ctypes.c_void_p()

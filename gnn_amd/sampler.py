@@ -16,6 +16,7 @@ reference's int16 would not have overflowed.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -307,6 +308,54 @@ def native_graph(lap) -> NativeGraph:
     return g
 
 
+class _ColCountApi(ctypes.Structure):
+    """gnn_colcount_api (include/gnn_sampler.h): libgnn_spmm.so's gnn_colcount_* by address."""
+    _fields_ = [("create", ctypes.c_void_p), ("add", ctypes.c_void_p), ("reset", ctypes.c_void_p),
+                ("destroy", ctypes.c_void_p), ("device", ctypes.c_int32), ("indptr", ctypes.c_void_p),
+                ("indices", ctypes.c_void_p)]
+
+
+def colcount_api(graph, device) -> "_ColCountApi":
+    """The device column-count API over the graph's DeviceGraph on `device` (made if needed)."""
+    from . import _lib
+
+    dg = device_graph(graph, device)
+    L = _lib.lib()
+    fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value
+    api = _ColCountApi(fp(L.gnn_colcount_create), fp(L.gnn_colcount_add), fp(L.gnn_colcount_reset),
+                       fp(L.gnn_colcount_destroy), dg.device.index if dg.device.index is not None else 0,
+                       dg.indptr.data_ptr(), dg.indices.data_ptr())
+    api._dg = dg  # the device arrays stay alive with the struct
+    return api
+
+
+class ColumnCounter:
+    """A device column-count context for calls from THIS thread (gnn_ladies_sample_cc): U's column
+    counts of the LADIES draw summed on the GPU; the draw and its outputs are unchanged."""
+
+    def __init__(self, graph, device):
+        from . import _lib
+
+        self.api = colcount_api(graph, device)
+        ctx = ctypes.c_void_p()
+        _lib.check(_lib.lib().gnn_colcount_create(self.api.device, native_graph(graph).num_nodes, self.api.indptr,
+                                                  self.api.indices, ctypes.byref(ctx)), "gnn_colcount_create")
+        self.ctx = ctx
+
+    def close(self) -> None:
+        from . import _lib
+
+        if self.ctx:
+            _lib.lib().gnn_colcount_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def extract_mask(device_extract) -> int:
     """device_extract (True = every layer below the top one, False / None = none, or an iterable
     of bottom-up layer indices) as the native samplers' layer mask (-1 = all)."""
@@ -321,14 +370,12 @@ def extract_mask(device_extract) -> int:
 
 
 def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders, kind: str = "ladies",
-                   csc_from: int = 1, device_extract=False):
+                   csc_from: int = 1, device_extract=False, colcount: "Optional[ColumnCounter]" = None):
     """Run gnn_ladies_sample / gnn_subgraph_sample / gnn_fastgcn_sample and copy the result
     out: (layers, sampled_nodes, input_nodes, pinned tensors). Layers >= csc_from (those
     whose input needs a gradient; layer 0's input is the features) also get their CSC.
     device_extract (LADIES; see extract_mask): those layers below the top one are left to the GPU
     extraction — only their rows, columns, segment offsets, CSC column pointer and nnz come back."""
-    import ctypes
-
     from . import _lib
 
     L = _lib.sampler_lib()
@@ -342,6 +389,11 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
     rest = (ptr(bn), bn.size, ptr(sn), ptr(od), nl, int(seed) & 0xFFFFFFFF, ctypes.byref(h))
     if kind == "fastgcn":
         rc = L.gnn_fastgcn_sample(*g3, ptr(graph.fastgcn_p), *rest)
+    elif kind == "ladies" and colcount is not None:
+        ipt = graph.transpose_structure[1] if device_extract else None
+        rc = L.gnn_ladies_sample_cc(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), ptr(ipt), graph.num_nodes,
+                                    *rest[:-1], extract_mask(device_extract), ctypes.byref(colcount.api), colcount.ctx,
+                                    rest[-1])
     elif kind == "ladies" and device_extract:
         ipt = graph.transpose_structure[1]
         rc = L.gnn_ladies_sample_dev(ptr(graph.indptr), ptr(graph.indices), ptr(graph.data), ptr(ipt), graph.num_nodes,
@@ -408,7 +460,8 @@ def _native_layers(seed, batch_nodes, samp_num_list, graph: NativeGraph, orders,
 def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, labels_full,
                        orders: Sequence[int], device_id_of_nodes, idx_of_nodes_on_device,
                        skewed_sampling_nodes=None, scale_factor: float = 1.0, devices=(0,),
-                       native: bool = True, device_extract=False) -> HostBatch:
+                       native: bool = True, device_extract=False,
+                       colcount: "Optional[ColumnCounter]" = None) -> HostBatch:
     """sampler.py:90-160 without the device work.
 
     native=True runs the C++ sampler (libgnn_sampler.so, bit-identical; releases the GIL, so
@@ -416,7 +469,8 @@ def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, 
     reference never reaches) runs the numpy restatement below. device_extract (native, a graph
     without stored zeros; True = every layer below the top one, or bottom-up layer indices):
     those layers are extracted on the GPU by ``to_device`` (gnn_ladies_extract_f32) instead of on
-    the host — same operands."""
+    the host — same operands. colcount (native): a ColumnCounter made on this thread — U's column
+    counts summed on the GPU, same batch."""
     batch_nodes = np.asarray(batch_nodes)
     if native and not scale_factor > 1:
         g = native_graph(lap_matrix)
@@ -424,7 +478,8 @@ def ladies_sample_host(seed, batch_nodes, samp_num_list, num_nodes, lap_matrix, 
             raise ValueError("num_nodes does not match lap_matrix")
         dx = device_extract if (extract_mask(device_extract) and g.data is None) else False
         layers, sampled_nodes, previous_nodes, pinned = _native_layers(seed, batch_nodes, samp_num_list, g,
-                                                                       list(orders), device_extract=dx)
+                                                                       list(orders), device_extract=dx,
+                                                                       colcount=colcount)
         hb = _finish_batch(layers, sampled_nodes, previous_nodes, batch_nodes, labels_full, device_id_of_nodes,
                            idx_of_nodes_on_device, devices, seed)
         lab = torch.from_numpy(hb.labels)

@@ -55,6 +55,24 @@ int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, int64_
                            const int32_t* colptr_t, int32_t* rowptr, int32_t* col, float* val, int32_t* rows_t,
                            float* val_t, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream);
 
+/* U's column counts for the LADIES draw on the GPU (reference sampler.py:116-122,
+ * pi = norm(U, ord=0, axis=0)), for a host sampler thread (gnn_sampler.h: gnn_colcount_api).
+ * A context belongs to ONE host thread: its own stream, a device count array over the graph's
+ * nodes, pinned result buffers. Unlike the rest of this library these calls synchronise with
+ * their own stream (the host draw needs the result) and gnn_colcount_create allocates.
+ * create: graph = the lap matrix's canonical CSR in device memory (as gnn_ladies_extract_f32;
+ *   no stored zeros), device = the HIP device it lives on.
+ * add: count the entries of lap rows rows[0..n) (host node ids; repeats count again) into the
+ *   context's counts, then return the non-zero columns: *bits = bitmap (host, ceil(N/64) words,
+ *   bit c%64 of word c/64), *counts = their counts in ascending column order (host, *nlive
+ *   entries). Both stay valid until the next call on the context.
+ * reset: zero the counts (stream-ordered before the next add). */
+int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx);
+int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, const uint64_t** bits,
+                     const int32_t** counts);
+int gnn_colcount_reset(void* ctx);
+void gnn_colcount_destroy(void* ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -56,6 +56,28 @@ int gnn_ladies_sample_dev(const int64_t* indptr, const int32_t* indices, const f
                           const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
                           gnn_ladies_result** out);
 
+/* Optional device column counting for the LADIES draw: libgnn_spmm.so's gnn_colcount_* entry
+ * points (include/gnn_extract.h), bound by address — this library stays free of the GPU runtime —
+ * and the graph's CSR in device memory (no stored zeros). With it U's column counts (the
+ * draw's p, sampler.py:116-122) are summed on the GPU from the rows each layer adds; the draw,
+ * and so every output, is unchanged. ctx: from create(device, num_nodes, indptr, indices, &ctx)
+ * on the calling thread (a context belongs to one thread). */
+typedef struct gnn_colcount_api {
+  int (*create)(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx);
+  int (*add)(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, const uint64_t** bits, const int32_t** counts);
+  int (*reset)(void* ctx);
+  void (*destroy)(void* ctx);
+  int32_t device;
+  const int64_t* indptr;  /* device */
+  const int32_t* indices; /* device */
+} gnn_colcount_api;
+
+/* gnn_ladies_sample_dev with U's column counts on the device (cc, cc_ctx; both NULL: on the host). */
+int gnn_ladies_sample_cc(const int64_t* indptr, const int32_t* indices, const float* data, const int64_t* indptr_t,
+                         int64_t num_nodes, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
+                         const int32_t* orders, int32_t num_layers, uint32_t seed, int32_t device_extract,
+                         const gnn_colcount_api* cc, void* cc_ctx, gnn_ladies_result** out);
+
 /* subgraph_sampler (sampler.py:7-88): ONE importance draw from the batch's neighbourhood
  * (same p, s_num = min(#(p > 0), samp_num[0]), same RNG use), after = unique(sampled ∪ batch);
  * the top-most layer with a non-zero order gets lap[batch, :][:, after]; every layer below it
@@ -165,6 +187,9 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
                               const int64_t* samp_num, const int32_t* orders, int32_t num_layers, int32_t kind,
                               const double* fastgcn_p, int32_t device_extract, int32_t csc_from, int32_t workers,
                               int32_t pinned);
+/* LADIES loaders: count U's columns on the device (each worker thread makes its own context on
+ * first use). Call before the first gnn_loader_submit; api is copied. */
+int gnn_loader_set_colcount(gnn_loader* ld, const gnn_colcount_api* api);
 /* Queue one batch (node ids copied); batches come out of gnn_loader_next in submission order. */
 int gnn_loader_submit(gnn_loader* ld, uint32_t seed, const int64_t* nodes, int64_t n);
 /* Block until the oldest submitted batch is ready. On a sampling error returns its status (the
@@ -182,6 +207,12 @@ void gnn_loader_destroy(gnn_loader* ld);
  * pinned buffer that one hipMemcpyAsync then moves to the GPU. */
 int gnn_host_gather_rows_f32(const float* src, int64_t ld_src, int64_t num_src_rows, const int64_t* idx, int64_t n,
                              int64_t F, float* dst, int64_t ld_dst);
+
+/* LADIES draw phase timers, summed over all threads since the last reset, when the process runs
+ * with GNN_SAMPLER_PROFILE=1 (returns 1 otherwise): out[0..n) = seconds in scratch reset, U's
+ * row pointer, U's column counts, the draw, unique(sampled ∪ prev), the extraction (or the
+ * device-layer metadata), normfact / positions; out[7] = calls. */
+int gnn_sampler_profile(double* out, int32_t n, int32_t reset);
 
 /* numpy legacy RandomState(seed).random_sample(n) — exposed for the RNG-stream tests. */
 int gnn_mt19937_random_sample(uint32_t seed, int64_t n, double* out);

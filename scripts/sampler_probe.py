@@ -13,6 +13,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gnn_amd import graphs, sampler  # noqa: E402
+from gnn_amd._lib import sampler_lib  # noqa: E402
 
 spec = {"reddit": graphs.REDDIT, "products": graphs.PRODUCTS, "papers": graphs.PAPERS_SCALED,
         "products-test": graphs.PRODUCTS_TEST}[sys.argv[1] if len(sys.argv) > 1 else "reddit"]
@@ -71,5 +72,9 @@ for kind in kinds:
             h.update(np.ascontiguousarray(s).tobytes())
         h.update(np.ascontiguousarray(inp).tobytes())
     ts = np.array(ts) * 1e3
+    prof = np.zeros(8)
+    if sampler_lib().gnn_sampler_profile(prof.ctypes.data, 8, 1) == 0 and prof[7] > 0:
+        names = ["scratch", "rowptr", "count", "draw", "after", "extract", "tail"]
+        print("  ms/call: " + " ".join(f"{nm} {1e3 * prof[i] / prof[7]:.2f}" for i, nm in enumerate(names)), flush=True)
     print(f"{kind}: {ts.mean():.2f} ms/batch (median {np.median(ts):.2f}, min {ts.min():.2f})  sha {h.hexdigest()[:16]}",
           flush=True)
