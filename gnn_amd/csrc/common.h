@@ -25,6 +25,14 @@ int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
                          const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
                          int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
 
+// gnn_gemm_f32_split3 with row-indexed operands: A's row m is A[ia[b][m]] (m-major A, a_rows
+// source rows), B's row k is B[ib[b][k]] (k-major B, b_rows source rows); NULL arrays / entries:
+// not indexed. Same sums as the split3 product of the gathered operands (gemm.hip).
+int gemm_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                        const float* const* A, int64_t lda, const int64_t* const* ia, int64_t a_rows,
+                        const float* const* B, int64_t ldb, const int64_t* const* ib, int64_t b_rows,
+                        float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+
 }  // namespace gnn
 
 #define GNN_REQUIRE(cond, ...)                              \

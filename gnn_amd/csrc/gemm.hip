@@ -51,6 +51,11 @@ struct Batch {
   const float* A[MAX_BATCH];
   const float* B[MAX_BATCH];
   float* C[MAX_BATCH];
+  // split3 only: row indices of A / B (NULL: none). An indexed operand's row r is the source's
+  // row idx[r] — A's rows m (m-major A) or B's rows k (k-major B): the GraphSAGE x[sampled]
+  // operand read in place instead of gathered first.
+  const int64_t* ia[MAX_BATCH];
+  const int64_t* ib[MAX_BATCH];
 };
 
 // Four consecutive floats of a row: one 16-byte load (VEC 4) or two 8-byte loads (VEC 2,
@@ -308,26 +313,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t s3_rsrc(const float* p, int64_
 //   k-major source: thread t holds column m = t & 127 (a wave instruction reads 64 consecutive
 //     floats of one k row); the k half kh = t >> 7 is wave-uniform.
 //   k-contiguous source: thread t holds row t >> 1, k half t & 1 (two 16-byte or four 8-byte loads).
-template <bool KMAJ, int VEC, bool GUARD>
+// IX (k-major sources): row k of the operand is the source's row idx[k] (a wave-uniform scalar
+// load per row); m-major sources take their row index in the fixed offset (s3_voff).
+template <bool KMAJ, int VEC, bool GUARD, bool IX = false>
 __device__ __forceinline__ void s3_load(__amdgpu_buffer_rsrc_t rs, const float* __restrict__ P, int64_t ld, int voff,
-                                        int r0, int rlim, int k0, int klim, int t, float v[8]) {
+                                        int r0, int rlim, int k0, int klim, int t, float v[8],
+                                        const int64_t* __restrict__ idx = nullptr) {
   if constexpr (KMAJ) {
     const int kb = k0 + __builtin_amdgcn_readfirstlane((t >> 7) * 8);
     if constexpr (GUARD) {
       const int m = min(r0 + (t & 127), rlim - 1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = (kb + i < klim) ? P[(int64_t)(kb + i) * ld + m] : 0.0f;
+      for (int i = 0; i < 8; ++i)
+        v[i] = (kb + i < klim) ? P[(IX ? idx[kb + i] : (int64_t)(kb + i)) * ld + m] : 0.0f;
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         v[i] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (int)((int64_t)(kb + i) * ld * 4), 0));
+            float, __builtin_amdgcn_raw_buffer_load_b32(
+                       rs, voff, (int)((IX ? idx[kb + i] : (int64_t)(kb + i)) * ld * 4), 0));
     }
   } else {
     if constexpr (GUARD) {
       const int m = min(r0 + (t >> 1), rlim - 1);
       const int kb = k0 + (t & 1) * 8;
-      const float* q = P + (int64_t)m * ld + kb;
+      const float* q = P + (IX ? idx[m] : (int64_t)m) * ld + kb;
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = (kb + i < klim) ? q[i] : 0.0f;
     } else {
@@ -351,9 +361,12 @@ __device__ __forceinline__ void s3_load(__amdgpu_buffer_rsrc_t rs, const float* 
 
 // The thread's fixed VGPR byte offset for s3_load (rows past the edge clamped to the last row).
 template <bool KMAJ>
-__device__ __forceinline__ int s3_voff(int64_t ld, int r0, int rlim, int t) {
+__device__ __forceinline__ int s3_voff(int64_t ld, int r0, int rlim, int t, const int64_t* __restrict__ idx = nullptr) {
   if constexpr (KMAJ) return min(r0 + (t & 127), rlim - 1) * 4;
-  else return (int)(((int64_t)min(r0 + (t >> 1), rlim - 1) * ld + (t & 1) * 8) * 4);
+  else {
+    const int r = min(r0 + (t >> 1), rlim - 1);
+    return (int)(((idx ? idx[r] : (int64_t)r) * ld + (t & 1) * 8) * 4);
+  }
 }
 
 // Offset (in bf16 units) of the 16-byte chunk (row, k half h) in a piece image. The half is
@@ -427,7 +440,7 @@ __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, co
 }
 
 // three workgroups per CU: LDS 48 KB each, registers capped at 168 (3 waves per SIMD)
-template <bool AK, bool BKM, int VA, int VB>
+template <bool AK, bool BKM, int VA, int VB, bool IDX = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
                                                          int64_t ldc, int splits, int klen, float* __restrict__ part,
                                                          int64_t abytes, int64_t bbytes, int xcd_map) {
@@ -460,7 +473,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const float* __restrict__ A = bt.A[b];
   const float* __restrict__ B = bt.B[b];
   const __amdgpu_buffer_rsrc_t rsa = s3_rsrc(A, abytes), rsb = s3_rsrc(B, bbytes);
-  const int voa = s3_voff<AK>(lda, m0, M, t), vob = s3_voff<BKM>(ldb, n0, N, t);
+  // IDX instantiations: A indexed when m-major, B when k-major (the two GraphSAGE x[sampled] uses)
+  const int64_t* __restrict__ ia = (IDX && !AK) ? bt.ia[b] : nullptr;
+  const int64_t* __restrict__ ib = (IDX && BKM) ? bt.ib[b] : nullptr;
+  const int voa = s3_voff<AK>(lda, m0, M, t, ia), vob = s3_voff<BKM>(ldb, n0, N, t);
 
   f16v acc[2][2];
 #pragma unroll
@@ -479,7 +495,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   auto load_ab = [&](int kt, float(&xa)[8], float(&xb)[8]) {
     const int k0 = kbeg + min(kt, nfull - 1) * S3_BK;
     s3_load<AK, VA, false>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
-    s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
+    if (IDX && BKM && ib)
+      s3_load<BKM, VB, false, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb, ib);
+    else
+      s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0, N, k0, kend, t, xb);
   };
   auto store_ab = [&](int stage, const float(&xa)[8], const float(&xb)[8]) {
     s3_store<AK>(As[stage], t, xa);
@@ -511,8 +530,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
   if (kbeg + nfull * S3_BK < kend) {  // k tail
     const int k0 = kbeg + nfull * S3_BK;
-    s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0]);
-    s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, rb[0]);
+    if (IDX && !AK && ia)
+      s3_load<AK, VA, true, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0], ia);
+    else
+      s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0]);
+    if (IDX && BKM && ib)
+      s3_load<BKM, VB, true, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, rb[0], ib);
+    else
+      s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0, N, k0, kend, t, rb[0]);
     store_ab(0, ra[0], rb[0]);
     __syncthreads();
     s3_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
@@ -566,9 +591,19 @@ int64_t slots_of(int algo) { return algo == ALGO_S3 ? SLOTS_S3 : SLOTS_F32; }
 
 // split_nbatch: the batch count the split-k choice is made for (0: nbatch). A product launched
 // alone with split_nbatch = n sums in exactly the order it would inside a batch of n.
+// Indexed operands (split3): ia / ib (per batch entry, NULL entries allowed) with the source's row
+// count a_rows / b_rows (its extent for the buffer range); A is indexable when m-major, B when
+// k-major.
+struct RowIndex {
+  const int64_t* const* ia = nullptr;
+  int64_t a_rows = 0;
+  const int64_t* const* ib = nullptr;
+  int64_t b_rows = 0;
+};
+
 int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
              int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
-             size_t workspace_bytes, void* stream, int split_nbatch = 0) {
+             size_t workspace_bytes, void* stream, int split_nbatch = 0, const RowIndex* ri = nullptr) {
   GNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gnn_gemm_f32: negative size");
   GNN_REQUIRE(M < INT_MAX && N < INT_MAX && K < INT_MAX, "gnn_gemm_f32: sizes must be < 2^31");
   GNN_REQUIRE(nbatch >= 1 && nbatch <= MAX_BATCH, "gnn_gemm_f32: nbatch must be 1..%d", MAX_BATCH);
@@ -587,11 +622,22 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
     bt.A[b] = A[b];
     bt.B[b] = B[b];
     bt.C[b] = C[b];
+    bt.ia[b] = ri && ri->ia ? ri->ia[b] : nullptr;
+    bt.ib[b] = ri && ri->ib ? ri->ib[b] : nullptr;
   }
+  bool idx = false;
+  for (int b = 0; b < nbatch; ++b) idx = idx || bt.ia[b] || bt.ib[b];
+  GNN_REQUIRE(!idx || (algo == ALGO_S3 && (!ri->ia || !a_kmajor) && (!ri->ib || b_kmajor)),
+              "gnn_gemm: row indices need split3, an m-major A or a k-major B");
   // split3 addresses operands by 32-bit buffer offsets: operands of >= 2 GiB take the f32-input kernel
-  const int64_t abytes = K == 0 ? 0 : ((a_kmajor ? K : M) - 1) * lda * 4 + (a_kmajor ? M : K) * 4;
-  const int64_t bbytes = K == 0 ? 0 : ((b_kmajor ? K : N) - 1) * ldb * 4 + (b_kmajor ? N : K) * 4;
-  if (algo == ALGO_S3 && (abytes >= INT_MAX || bbytes >= INT_MAX)) algo = ALGO_F32;
+  const int64_t arows = (ri && ri->ia) ? ri->a_rows : (a_kmajor ? K : M);
+  const int64_t brows = (ri && ri->ib) ? ri->b_rows : (b_kmajor ? K : N);
+  const int64_t abytes = K == 0 ? 0 : (arows - 1) * lda * 4 + (a_kmajor ? M : K) * 4;
+  const int64_t bbytes = K == 0 ? 0 : (brows - 1) * ldb * 4 + (b_kmajor ? N : K) * 4;
+  if (algo == ALGO_S3 && (abytes >= INT_MAX || bbytes >= INT_MAX)) {
+    GNN_REQUIRE(!idx, "gnn_gemm: indexed operand of >= 2 GiB");
+    algo = ALGO_F32;
+  }
   hipStream_t st = (hipStream_t)stream;
   const int splits = K == 0 ? 1 : pick_splits(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch, slots_of(algo));
   // XCD-aware tile map for split3 (2-8 % per layer pair, scripts/gemm_bench.py); GNN_GEMM_XCD=0 turns it off
@@ -610,7 +656,11 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   float* part = (float*)workspace;
 #define GNN_GEMM_LAUNCH(AK, BK, VA, VB)                                                                     \
   do {                                                                                                        \
-    if (algo == ALGO_S3)                                                                                      \
+    if (algo == ALGO_S3 && idx)                                                                               \
+      gemm_s3_kernel<AK, BK, VA, VB, true><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb,  \
+                                                                       ldc, splits, klen, part, abytes, bbytes, \
+                                                                       xcdm);                                   \
+    else if (algo == ALGO_S3)                                                                                 \
       gemm_s3_kernel<AK, BK, VA, VB><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc,  \
                                                                  splits, klen, part, abytes, bbytes, xcdm);   \
     else if (bkt == 16)                                                                                       \
@@ -692,6 +742,19 @@ int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64
                          int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
   return gemm_run(ALGO_S3, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
                   stream, split_nbatch);
+}
+
+int gemm_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                        const float* const* A, int64_t lda, const int64_t* const* ia, int64_t a_rows,
+                        const float* const* B, int64_t ldb, const int64_t* const* ib, int64_t b_rows,
+                        float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+  RowIndex ri;
+  ri.ia = ia;
+  ri.a_rows = a_rows;
+  ri.ib = ib;
+  ri.b_rows = b_rows;
+  return gemm_run(ALGO_S3, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
+                  stream, 0, &ri);
 }
 
 }  // namespace gnn

@@ -151,6 +151,15 @@ int fork_join(Aux* a, hipStream_t from, hipStream_t to) {
 // GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
 // step it changed nothing (550 mini-batches/s either way; the layer-0/1 aggregations slowed from
 // 239 to 261 us while the GEMMs ran beside them — the CUs are already saturated).
+// GNN_STEP_GATHER=1: gather x[sampled] first even where the GEMMs could read it in place (A/B)
+bool no_index() {
+  static const bool on = [] {
+    const char* e = getenv("GNN_STEP_GATHER");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
+
 bool overlap_enabled() {
   static const bool on = [] {
     const char* e = getenv("GNN_STEP_OVERLAP");
@@ -187,6 +196,7 @@ int mm_gtx(rocblas_handle h, const float* g, int64_t ldg, const float* x, int64_
 // The per-layer buffers of one step (carved in a fixed order: sizing and running share it).
 struct LayerBufs {
   int64_t M, K, nnz, F, Fk, ldx, ldo, N, D;
+  bool xs_gathered;  // false: x[sampled] is read in place by the split3 GEMMs (row-indexed X)
   const float* X;
   float *feat, *xs, *hB, *hW, *Y, *mean, *rstd;
   float *dY, *dhB, *dhW, *dxs, *dfeat;
@@ -360,6 +370,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     if (aux && pl.sage && ok && fills(b.M, N, n)) {
       // x[sampled] and linearB on the aux stream beside A·X and linearW; each product launched
       // alone with the split choice of the pair, so the sums are those of the batched launch
+      b.xs_gathered = true;
       GNN_TRY(fork_join(aux, st, aux->s));
       GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M, b.F,
                                   aux->s));
@@ -382,12 +393,23 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
                                P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
                                b.ws_fwd, b.b_fwd, 0, st));
-      if (pl.sage)
+      // x[sampled] feeds only linearB and its weight gradient: when both run on split3 (and X's
+      // rows have the aggregation output's stride) the GEMMs read X's rows through the index
+      // instead of a gathered copy (bit-identical operands)
+      b.xs_gathered = !(pl.sage && ok && fills(b.M, N, n) && b.M >= 2048 && b.ldx == b.ldo && !no_index());
+      if (pl.sage && b.xs_gathered)
         GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M,
                                     b.F, st));
     }
     if (aux && pl.sage && ok && fills(b.M, N, n)) {
       // done above
+    } else if (ok && fills(b.M, N, n) && !b.xs_gathered) {
+      const float* A[2] = {b.X, b.feat};
+      const int64_t* IA[2] = {P<const int64_t>(d, l, GNN_SL_SAMPLED), nullptr};
+      const float* B[2] = {WB, WW};
+      float* Cc[2] = {b.hB, b.hW};
+      GNN_TRY(gnn::gemm_split3_indexed(0, 0, b.M, N, b.F, n, A, b.ldo, IA, b.K, B, b.F, nullptr, 0, Cc, N,
+                                       b.ws_gemm_f, b.b_gemm_f, st));
     } else if (ok && fills(b.M, N, n)) {
       const float* A[2] = {pl.sage ? b.xs : b.feat, b.feat};
       const float* B[2] = {pl.sage ? WB : WW, WW};
@@ -450,7 +472,8 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     float* gWB = pl.sage ? P<float>(d, l, GNN_SL_GWB) : nullptr;
     float* gWW = P<float>(d, l, GNN_SL_GWW);
     if (ok && b.M >= 2048) {
-      const float* X[2] = {pl.sage ? b.xs : b.feat, b.feat};
+      const float* X[2] = {pl.sage ? (b.xs_gathered ? b.xs : b.X) : b.feat, b.feat};
+      const int64_t* IB[2] = {pl.sage && !b.xs_gathered ? P<const int64_t>(d, l, GNN_SL_SAMPLED) : nullptr, nullptr};
       float* Cc[2] = {pl.sage ? gWB : gWW, gWW};
       hipStream_t sw = st;
       if (aux && l >= 1) {
@@ -458,8 +481,12 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
         sw = aux->s;
         aux_used = true;
       }
-      GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
-                                  b.b_gemm_dw, sw));
+      if (pl.sage && !b.xs_gathered)
+        GNN_TRY(gnn::gemm_split3_indexed(1, 1, N, b.F, b.M, n, G + o, N, nullptr, 0, X + o, b.ldo, IB + o, b.K,
+                                         Cc + o, b.F, b.ws_gemm_dw, b.b_gemm_dw, sw));
+      else
+        GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
+                                    b.b_gemm_dw, sw));
     } else {
       if (pl.sage) GNN_TRY(mm_gtx(h, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
       GNN_TRY(mm_gtx(h, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
