@@ -81,6 +81,8 @@ _SIGNATURES = {
     "gnn_gemm_f32_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
     "gnn_gemm_f32": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ, _VP]),
     "gnn_gemm_f32_split3_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
+    "gnn_gemm_f32_split3_indexed": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP,
+                                           _I64, _VP, _I64, _VP, _SZ, _VP]),
     "gnn_gemm_f32_split3": (_INT, [_INT, _INT, _I64, _I64, _I64, _INT, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _SZ,
                                    _VP]),
 }

@@ -733,6 +733,15 @@ int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_
                   stream);
 }
 
+int gnn_gemm_f32_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                                const float* const* A, int64_t lda, const int64_t* const* ia, int64_t a_rows,
+                                const float* const* B, int64_t ldb, const int64_t* const* ib, int64_t b_rows,
+                                float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+  GNN_REQUIRE((!ia || a_rows > 0) && (!ib || b_rows > 0), "gnn_gemm_f32_split3_indexed: source rows");
+  return gnn::gemm_split3_indexed(a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, ia, a_rows, B, ldb, ib, b_rows, C, ldc,
+                                  workspace, workspace_bytes, stream);
+}
+
 }  // extern "C"
 
 namespace gnn {

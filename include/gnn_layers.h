@@ -70,6 +70,15 @@ int gnn_gemm_f32_split3(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_
                         const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
                         int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
 
+/* gnn_gemm_f32_split3 with row-indexed operands: row m of an m-major A is A[ia[b][m]] (a_rows
+ * source rows), row k of a k-major B is B[ib[b][k]] (b_rows source rows); ia / ib or entries NULL
+ * = not indexed (an indexed k-major A or m-major B is rejected). Bit-identical to the split3
+ * product of the gathered operands — GraphSAGE's x[sampled] (models.py:18-21) read in place. */
+int gnn_gemm_f32_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,
+                                const float* const* A, int64_t lda, const int64_t* const* ia, int64_t a_rows,
+                                const float* const* B, int64_t ldb, const int64_t* const* ib, int64_t b_rows,
+                                float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Classifier head + loss (head.hip). Replaces GNN.forward's tail (models.py:90-97:
  * F.normalize(x, 2, 1) -> dropout(p) -> nn.Linear(D, C)) and utils.loss with sigmoid_loss

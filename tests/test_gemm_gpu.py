@@ -101,3 +101,65 @@ def test_linear_pair_matches_torch(dev, n):
         np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(), rtol=1e-4, atol=2e-4)
     for a, b in zip(xs + Ws, xr + Wr):
         np.testing.assert_allclose(a.grad.cpu().numpy(), b.grad.cpu().numpy(), rtol=1e-4, atol=2e-3)
+
+
+def _ptrs(ts):
+    import ctypes
+
+    arr = (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+    return arr
+
+
+@pytest.mark.parametrize("case", ["a_fwd", "b_wgrad"])
+@pytest.mark.parametrize("M,N,K,R", [(4100, 512, 602, 6000), (300, 130, 77, 1000), (513, 1024, 1024, 800)])
+def test_split3_row_indexed_equals_gathered(dev, case, M, N, K, R):
+    """gnn_gemm_f32_split3_indexed: an m-major A (the forward's x[sampled]) or a k-major B (the
+    weight gradient's x[sampled]) read through a row index (repeats allowed) gives exactly the
+    split3 product of the gathered operand — same bits, batched with an unindexed product."""
+    from gnn_amd import _lib
+    from gnn_amd.fused import gemm
+
+    g = torch.Generator().manual_seed(M + N + K)
+    L = _lib.lib()
+    if case == "a_fwd":  # C (M x N) = A[idx] (M x K) · Bᵀ, B (N x K)
+        src = torch.randn(R, K + (K & 1), generator=g).to(dev)
+        idx = torch.randint(0, R, (M,), generator=g).to(dev)
+        other = torch.randn(M, src.shape[1], generator=g).to(dev)
+        Bw = torch.randn(N, K + (K & 1), generator=g).to(dev)
+        A_ref = [src[idx][:, :K], other[:, :K]]
+        ref = gemm(False, False, A_ref, [Bw[:, :K], Bw[:, :K]], M, N, K, algo="split3")
+        out = [torch.empty(M, N, device=dev) for _ in range(2)]
+        wsb = L.gnn_gemm_f32_split3_workspace_bytes(M, N, K, 2)
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        # the indexed source and the plain operand share the row stride
+        rc = L.gnn_gemm_f32_split3_indexed(0, 0, M, N, K, 2, _ptrs([src, other]), src.stride(0),
+                                           _ptrs([idx, None]), R, _ptrs([Bw, Bw]), Bw.stride(0), None, 0,
+                                           _ptrs(out), N, ws.data_ptr(), wsb, _lib.stream_of(dev))
+    else:  # C (N x K) = Gᵀ (G: M x N, k-major over M) · X[idx] (M x K, k-major B)
+        src = torch.randn(R, K + (K & 1), generator=g).to(dev)
+        idx = torch.randint(0, R, (M,), generator=g).to(dev)
+        other = torch.randn(M, src.shape[1], generator=g).to(dev)
+        G = torch.randn(M, N + (N & 1), generator=g).to(dev)
+        ref = gemm(True, True, [G[:, :N], G[:, :N]], [src[idx][:, :K], other[:, :K]], N, K, M, algo="split3")
+        out = [torch.empty(N, K, device=dev) for _ in range(2)]
+        wsb = L.gnn_gemm_f32_split3_workspace_bytes(N, K, M, 2)
+        ws = torch.empty(max(wsb, 256), dtype=torch.uint8, device=dev)
+        rc = L.gnn_gemm_f32_split3_indexed(1, 1, N, K, M, 2, _ptrs([G, G]), G.stride(0), None, 0,
+                                           _ptrs([src, other]), src.stride(0), _ptrs([idx, None]), R,
+                                           _ptrs(out), K, ws.data_ptr(), wsb, _lib.stream_of(dev))
+    assert rc == 0, L.gnn_last_error()
+    torch.cuda.synchronize()
+    for c, r in zip(out, ref):
+        assert torch.equal(c, r)
+
+
+def test_split3_indexed_rejects_bad_layouts(dev):
+    from gnn_amd import _lib
+
+    L = _lib.lib()
+    a = torch.zeros(64, 64, device=dev)
+    idx = torch.zeros(64, dtype=torch.int64, device=dev)
+    c = torch.empty(64, 64, device=dev)
+    rc = L.gnn_gemm_f32_split3_indexed(1, 0, 64, 64, 64, 1, _ptrs([a]), 64, _ptrs([idx]), 64, _ptrs([a]), 64, None, 0,
+                                       _ptrs([c]), 64, None, 0, _lib.stream_of(dev))
+    assert rc != 0 and b"row indices" in L.gnn_last_error()
