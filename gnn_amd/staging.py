@@ -26,7 +26,9 @@ Here (DESIGN.md §Feature staging):
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import sys
 import weakref
 from dataclasses import dataclass
 from typing import List, Optional
@@ -312,6 +314,20 @@ class NegotiatedStream:
         self.pool.shutdown(wait=True)
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Send file descriptor 1 to stderr for the duration (native libraries' prints included)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class PeerExchange:
     """All-to-all exchange of buffered rows held by peer GPUs (RCCL over xGMI).
 
@@ -335,7 +351,8 @@ class PeerExchange:
             # always a group of its own: the negotiation may run on another thread
             # (NegotiatedStream) while this thread's row all-to-all / gradient all-reduce use
             # `group` — two threads on one communicator would interleave their collectives
-            meta_group = dist.new_group(backend="gloo")
+            with stdout_to_stderr():  # gloo prints its connection lines on stdout (bench: one JSON line)
+                meta_group = dist.new_group(backend="gloo")
         self.meta_group = meta_group
 
     def prepare(self, plan: StagePlan) -> tuple:

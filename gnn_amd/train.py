@@ -141,5 +141,8 @@ def init_distributed(backend: Optional[str] = None):
         if be == "nccl":
             torch.distributed.init_process_group(be, device_id=torch.device("cuda", local))
         else:
-            torch.distributed.init_process_group(be)
+            from .staging import stdout_to_stderr
+
+            with stdout_to_stderr():  # gloo's connection lines go to stderr, not into the bench's stdout
+                torch.distributed.init_process_group(be)
     return rank, world, local
