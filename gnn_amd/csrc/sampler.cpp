@@ -235,6 +235,7 @@ class Work {
       tw->counted_list.clear();
       tw->live.clear();
       tw->found.clear();
+      tw->has_live_cnt = false;
     }
     tw->clean_ = false;
     return *tw;
@@ -299,27 +300,35 @@ class Work {
     const int32_t* counts = nullptr;
     *rc = cc->add(ctx, send->data(), (int64_t)send->size(), &nlive, &bits, &counts);
     if (*rc) return -1;
-    live.clear();
-    live.reserve((size_t)nlive);
-    int64_t isum = 0, i = 0;
+    // live from the bitmap, cnt[live] from the counts (ascending stores); the counts also stay
+    // contiguous in live order for the draw's p (choose_by_counts)
+    live.resize((size_t)nlive);
+    live_cnt.assign(counts, counts + nlive);
+    int64_t* const lp = live.data();
+    int32_t* const cp = cnt.data();
+    int64_t i = 0;
     const size_t W = (g_.N + 63) / 64;
     for (size_t wi = 0; wi < W; ++wi) {
-      for (uint64_t x = bits[wi]; x; x &= x - 1) {
+      uint64_t x = bits[wi];
+      if (!x) continue;
+      if (i + __builtin_popcountll(x) > nlive) {
+        *rc = -5;
+        return -1;
+      }
+      for (; x; x &= x - 1) {
         const size_t c = (wi << 6) + (size_t)__builtin_ctzll(x);
-        if (i >= nlive || c >= g_.N) {
-          *rc = -5;
-          return -1;
-        }
-        cnt[c] = counts[i];
-        isum += counts[i];
-        live.push_back((int64_t)c);
+        lp[i] = (int64_t)c;
+        cp[c] = counts[i];
         ++i;
       }
     }
-    if (i != nlive) {
+    if (i != nlive || (nlive > 0 && (size_t)lp[nlive - 1] >= g_.N)) {
       *rc = -5;
       return -1;
     }
+    int64_t isum = 0;
+    for (int64_t k = 0; k < nlive; ++k) isum += counts[k];
+    has_live_cnt = true;
     return isum;
   }
 
@@ -338,6 +347,7 @@ class Work {
   // step compared at once; only the non-zero ones are visited (no per-column branch).
   int64_t scan_counts() {
     int64_t isum = 0;
+    has_live_cnt = false;
     live.clear();
     const int32_t* const c32 = cnt.data();
     const size_t N = g_.N, N16 = N & ~(size_t)15;
@@ -376,11 +386,21 @@ class Work {
     pv.resize(n);
     if (cdf_work.size() < n) cdf_work.resize(n);
     double s = 0.0;
-    for (size_t i = 0; i < n; ++i) {
-      const double q = (double)cnt[(size_t)live[i]] / total;
-      pv[i] = q;
-      s += q;
-      cdf_work[i] = s;
+    if (has_live_cnt) {  // device counts: already contiguous in live order
+      const int32_t* lc = live_cnt.data();
+      for (size_t i = 0; i < n; ++i) {
+        const double q = (double)lc[i] / total;
+        pv[i] = q;
+        s += q;
+        cdf_work[i] = s;
+      }
+    } else {
+      for (size_t i = 0; i < n; ++i) {
+        const double q = (double)cnt[(size_t)live[i]] / total;
+        pv[i] = q;
+        s += q;
+        cdf_work[i] = s;
+      }
     }
     choice_without_replacement(rng, live.data(), pv.data(), true, cdf_work.data(), n, s_num, taken, found, cdf_work,
                                xs, js);
@@ -545,6 +565,8 @@ class Work {
   std::vector<int64_t> live, found, counted_list, newrows;
   std::vector<double> pv, cdf_work, xs;  // choice scratch
   std::vector<uint32_t> js;
+  std::vector<int32_t> live_cnt;  // cnt[live[i]] in live order (device counts)
+  bool has_live_cnt = false;
   std::vector<int64_t> fg_live;          // FastGCN candidates (see choose_by_p)
   std::vector<double> fg_pv, fg_base;
   const double* fg_p = nullptr;

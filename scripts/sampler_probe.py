@@ -49,8 +49,11 @@ for kind in kinds:
         g = sampler.native_graph(graphs.lap_matrix(A, model))
         if cpath and model == "graphsage" and not os.path.exists(cpath):
             np.savez(cpath, indptr=g.indptr, indices=g.indices, train=np.asarray(train))
-    if kind == "ladies-dx":
+    cc = None
+    if kind.startswith("ladies-dx"):
         g.transpose_structure
+    if kind == "ladies-dx-cc":  # U's column counts on the GPU (needs a GPU)
+        cc = sampler.ColumnCounter(g, "cuda:0")
     if kind == "fastgcn":
         g.fastgcn_p
     h = hashlib.sha256()
@@ -59,7 +62,7 @@ for kind in kinds:
         t = time.perf_counter()
         layers, sampled, inp, _ = sampler._native_layers(1000 + i, b, [8192] * 3, g, [1, 1, 1],
                                                          kind="fastgcn" if kind == "fastgcn" else "ladies",
-                                                         device_extract=kind == "ladies-dx")
+                                                         device_extract=kind.startswith("ladies-dx"), colcount=cc)
         dt = time.perf_counter() - t
         if i >= 2:
             ts.append(dt)
