@@ -580,19 +580,22 @@ def main():
             return pre[j].plan, lambda: (db.build_operands(), db)[1]
 
         pipeline(nxt_pre, nwarm)
+        recs = []
+        if not args.no_roofline:
+            # the aggregation launches timed with HIP events recorded on their stream, over a timed
+            # pass of the distinct batches (the events cost ~3-5 % of the step, so the gpu_step
+            # value comes from a second pass over the same batches without them)
+            cso.enable_timing(True)
+            timed(lambda: pipeline(nxt_pre, gsteps))
+            cso.enable_timing(False)
+            recs = cso.take_timing_records()
+            k_[0] = nwarm
+            if native:  # the second pass rebuilds the device batches
+                for j in range(len(dbs)):
+                    dbs[j] = None
         stager.timing = []
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
         h_bytes, h_sec = stager.take_timing()
-        recs = []
-        if not args.no_roofline:
-            # the aggregation launches timed with HIP events in a second pass over the same
-            # batches (the per-launch events cost ~2-3 % of the step, so not in the timed pass)
-            k_[0] = nwarm
-            cso.enable_timing(True)
-            pipeline(nxt_pre, gsteps)
-            torch.cuda.synchronize()
-            cso.enable_timing(False)
-            recs = cso.take_timing_records()
         gpu_step = {"value": round(world * gsteps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / gsteps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / gsteps, 3),
