@@ -14,7 +14,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgnn_spmm.so")
+LIB_PATH = os.environ.get("GNN_SPMM_LIBRARY") or os.path.join(_HERE, "libgnn_spmm.so")  # override: experiments
 
 _lock = threading.Lock()
 _lib = None

@@ -1170,7 +1170,10 @@ WorkMap work_map(const SpmmCfg& c, int64_t M) {
 using MainFn = void (*)(const int*, const int*, const float*, int, int, int, int, const float*, int64_t,
                         float*, int64_t, float*, int64_t, int, const float*, int64_t, const int*, WorkMap);
 
-constexpr int pick_u(int nj) { return nj <= 4 ? 4 : (nj == 5 ? 3 : 2); }
+#ifndef GNN_SPMM_U1  // nonzeros in flight per lane group for one column chunk (experiments: -DGNN_SPMM_U1=n)
+#define GNN_SPMM_U1 4
+#endif
+constexpr int pick_u(int nj) { return nj <= 1 ? GNN_SPMM_U1 : (nj <= 4 ? 4 : (nj == 5 ? 3 : 2)); }
 
 template <int VW, int G, int NJ>
 MainFn main_ptr(bool res) {
