@@ -808,7 +808,9 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
   *out = nullptr;
   try {
     const Graph g{indptr, indices, data, (size_t)num_nodes};
+    PhaseClock clk;
     Work& w = Work::acquire(g);
+    if (g_prof_on) g_prof[P_CALLS].fetch_add(1, std::memory_order_relaxed);
     std::unique_ptr<gnn_ladies_result> res(new gnn_ladies_result());
     res->layers.resize((size_t)num_layers);
     MT19937 rng(seed);
@@ -817,10 +819,13 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
       Layer& L = res->layers[(size_t)(num_layers - 1 - d)];
       if (orders[num_layers - 1 - d] == 0) continue;
       L.present = true;
+      clk.lap(P_TAIL);
       const int64_t unnz = w.row_pointers(prev, L.fullrowptr);  // U = lap[prev, :]
+      clk.lap(P_ROWPTR);
       if (unnz < 0) return fail("gnn_fastgcn_sample: sub-graph nnz >= 2^31");
       // the layer-independent importance: candidates = ascending nodes with p > 0
       w.choose_by_p(rng, p, samp_num[d]);
+      clk.lap(P_DRAW);
       const int64_t s_num = std::min<int64_t>((int64_t)w.fastgcn_candidates(), samp_num[d]);
       L.s_num = s_num;
       // after = unique(sampled): layers are sampled independently (no union with prev)
@@ -828,7 +833,9 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
       std::sort(after.begin(), after.end());
       for (int64_t v : w.found) w.taken[(size_t)v] = 0;
       w.set_columns(after);
+      clk.lap(P_AFTER);
       w.extract(prev, unnz, L);
+      clk.lap(P_EXTRACT);
       Work::normfact_p(after, p, s_num, L);
       w.positions(after, prev, L);
       L.M = (int64_t)prev.size();
