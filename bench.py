@@ -99,6 +99,9 @@ def parse():
                          "(gnn_colcount_*, the graph resident in HBM); the draw itself stays on the host. auto: "
                          "gpu from 1 M nodes (A/B on one box: ogbn-products-shaped 363 -> 720 mini-batches/s end "
                          "to end; Reddit-shaped 558 host vs 516 gpu, where the host draw is not the bound)")
+    ap.add_argument("--numa", default="off", choices=["gpu", "off"],
+                    help="confine the process (training + producer threads) to the CPUs of the GPU's NUMA node "
+                         "(A/B on one box, 3 runs each: 572 vs 584 mini-batches/s unpinned, so off by default)")
     ap.add_argument("--python-loader", action="store_true",
                     help="batch producer: Python worker threads calling the native sampler (BatchLoader) instead of "
                          "the C++ producer (NativeLoader: GIL-free workers, one blob and one H2D per batch)")
@@ -254,6 +257,28 @@ def cpu_baseline(args, hb, feats, num_classes):
             "sample": f"{n} full GraphSAGE training steps (torch.sparse.mm fwd/bwd, dense layers, Adam) on "
                       f"pre-sampled batch 0 (samp {args.samp_num}, bs {args.batch_size}), {dt:.1f} s",
             "spmm_call_ms": calls}
+
+
+def gpu_numa_cpus(dev) -> list:
+    """The host CPUs of the GPU's NUMA node (sysfs; [] if unknown): the producer threads' blobs
+    and the training thread's launches then stay on the socket the GPU hangs off."""
+    try:
+        p = torch.cuda.get_device_properties(dev)
+        bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+        with open(f"/sys/bus/pci/devices/{bdf}/numa_node") as f:
+            node = int(f.read().strip())
+        if node < 0:
+            return []
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            spec = f.read().strip()
+        cpus = []
+        for part in spec.split(","):
+            a, _, b = part.partition("-")
+            cpus.extend(range(int(a), int(b or a) + 1))
+        allowed = os.sched_getaffinity(0)
+        return [c for c in cpus if c in allowed]
+    except (OSError, ValueError, AttributeError):
+        return []
 
 
 def cpu_budget() -> int:
@@ -434,6 +459,10 @@ def main():
     rank, world, local = init_distributed()
     assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE {world}"
     dev = torch.device("cuda", local)
+    numa_cpus = gpu_numa_cpus(dev) if args.numa == "gpu" else []
+    if len(numa_cpus) >= 4:
+        os.sched_setaffinity(0, numa_cpus)  # before any worker thread exists: they inherit it
+        log(f"pinned to the GPU's NUMA node: {len(numa_cpus)} CPUs")
     k = int(args.buffer_size * N)
     pl = placement.create_buffer(lap, train, k, list(range(world)), 3, alpha=0)
     pdev, pidx = pl.device_id_of_nodes_group[rank], pl.idx_of_nodes_on_device_group[rank]
@@ -676,7 +705,7 @@ def main():
                        "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
-                       "sampler_workers_per_rank": workers,
+                       "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
                        "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host",
                        "column_counts": "gpu" if getattr(loader, "device_count", False) else "host"},
