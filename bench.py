@@ -62,7 +62,7 @@ SAMPLERS = {"ladies": sampler.ladies_sample_host, "subgraph": sampler.subgraph_s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--gpu-step-batches", type=int, default=60,
                     help="distinct pre-sampled batches timed for the gpu_step field (at most --steps)")
