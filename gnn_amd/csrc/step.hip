@@ -148,9 +148,6 @@ int fork_join(Aux* a, hipStream_t from, hipStream_t to) {
   return 0;
 }
 
-// GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
-// step it changed nothing (550 mini-batches/s either way; the layer-0/1 aggregations slowed from
-// 239 to 261 us while the GEMMs ran beside them — the CUs are already saturated).
 // GNN_STEP_GATHER=1: gather x[sampled] first even where the GEMMs could read it in place (A/B)
 bool no_index() {
   static const bool on = [] {
@@ -160,6 +157,9 @@ bool no_index() {
   return on;
 }
 
+// GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
+// step it changed nothing (550 mini-batches/s either way; the layer-0/1 aggregations slowed from
+// 239 to 261 us while the GEMMs ran beside them — the CUs are already saturated).
 bool overlap_enabled() {
   static const bool on = [] {
     const char* e = getenv("GNN_STEP_OVERLAP");
