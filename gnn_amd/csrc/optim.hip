@@ -35,6 +35,10 @@ struct TensorList {
   int count;
 };
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bool aligned16(const void* q) { return ((uintptr_t)q & 15u) == 0; }
+
 __device__ __forceinline__ int tensor_of(const TensorList& L, int64_t chunk) {
   int i = 0;
   while (i + 1 < L.count && L.chunk0[i + 1] <= chunk) ++i;  // <= 32 entries, uniform
@@ -60,9 +64,14 @@ __global__ __launch_bounds__(256) void grad_sqnorm_kernel(TensorList L, float* _
   const int64_t end = min(base + (int64_t)CHUNK, L.n[i]);
   const float* g = L.g[i];
   float s = 0.0f;
-  for (int64_t e = base + threadIdx.x; e < end; e += 256) {
-    const float x = g[e];
-    s = fmaf(x, x, s);
+  if (end - base == CHUNK && aligned16(g + base)) {  // full chunk: one float4 per thread
+    const f4 x = reinterpret_cast<const f4*>(g + base)[threadIdx.x];
+    s = fmaf(x.w, x.w, fmaf(x.z, x.z, fmaf(x.y, x.y, x.x * x.x)));
+  } else {
+    for (int64_t e = base + threadIdx.x; e < end; e += 256) {
+      const float x = g[e];
+      s = fmaf(x, x, s);
+    }
   }
   const float t = block_sum(s, red);
   if (threadIdx.x == 0) partial[chunk] = t;
@@ -106,18 +115,38 @@ __global__ __launch_bounds__(256) void adam_kernel(TensorList L, const float* __
   const float* __restrict__ g = L.g[i];
   float* __restrict__ m = L.m[i];
   float* __restrict__ v = L.v[i];
+  // torch (_fused_adam / _multi_tensor_adam, amsgrad=False, weight_decay=0):
+  //   m = lerp(m, g, 1 - beta1); v = beta2 * v + (1 - beta2) * g * g
+  //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+  auto upd = [&](float gr, float mo, float vo, float po, float& mn, float& vn, float& pn) {
+    mn = mo + (1.0f - beta1) * (gr - mo);
+    vn = beta2 * vo + (1.0f - beta2) * gr * gr;
+    const float denom = sqrtf(vn) / bc2_sqrt + eps;
+    pn = po - step_size * (mn / denom);
+  };
+  if (end - base == CHUNK && aligned16(p + base) && aligned16(g + base) && aligned16(m + base) &&
+      aligned16(v + base)) {  // full chunk: one float4 of each stream per thread (same per-element math)
+    const int64_t e = base + 4 * threadIdx.x;
+    const f4 g4 = *reinterpret_cast<const f4*>(g + e) * sc;
+    const f4 m4 = *reinterpret_cast<const f4*>(m + e);
+    const f4 v4 = *reinterpret_cast<const f4*>(v + e);
+    const f4 p4 = *reinterpret_cast<const f4*>(p + e);
+    float mn[4], vn[4], pn[4];
+    upd(g4.x, m4.x, v4.x, p4.x, mn[0], vn[0], pn[0]);
+    upd(g4.y, m4.y, v4.y, p4.y, mn[1], vn[1], pn[1]);
+    upd(g4.z, m4.z, v4.z, p4.z, mn[2], vn[2], pn[2]);
+    upd(g4.w, m4.w, v4.w, p4.w, mn[3], vn[3], pn[3]);
+    *reinterpret_cast<f4*>(m + e) = f4{mn[0], mn[1], mn[2], mn[3]};
+    *reinterpret_cast<f4*>(v + e) = f4{vn[0], vn[1], vn[2], vn[3]};
+    *reinterpret_cast<f4*>(p + e) = f4{pn[0], pn[1], pn[2], pn[3]};
+    return;
+  }
   for (int64_t e = base + threadIdx.x; e < end; e += 256) {
-    const float gr = g[e] * sc;
-    // torch (_fused_adam / _multi_tensor_adam, amsgrad=False, weight_decay=0):
-    //   m = lerp(m, g, 1 - beta1); v = beta2 * v + (1 - beta2) * g * g
-    //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
-    const float mo = m[e];
-    const float mn = mo + (1.0f - beta1) * (gr - mo);
-    const float vn = beta2 * v[e] + (1.0f - beta2) * gr * gr;
+    float mn, vn, pn;
+    upd(g[e] * sc, m[e], v[e], p[e], mn, vn, pn);
     m[e] = mn;
     v[e] = vn;
-    const float denom = sqrtf(vn) / bc2_sqrt + eps;
-    p[e] = p[e] - step_size * (mn / denom);
+    p[e] = pn;
   }
 }
 

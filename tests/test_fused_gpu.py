@@ -235,3 +235,71 @@ def test_gpu_forward_loss_matches_reference(dev, golden, name):
     for pname, prm in net.named_parameters():
         np.testing.assert_allclose(prm.grad.cpu().numpy(), st[f"{name}_grad_{pname}"], rtol=2e-3, atol=1e-5,
                                    err_msg=pname)
+
+
+def _keep_mask_ref(seed, e, p):
+    """Per-element dropout keep mask of the layer tail, restated in numpy from its definition
+    (sage.hip `drop4`): h = mix32(lo32(e) ^ mix32(hi32(e) ^ mix32(lo32(seed) ^ 0x9e3779b9) ^
+    hi32(seed))), keep = float(h >> 8) * 2^-24 >= p."""
+    def mix32(x):
+        x = x.astype(np.uint64) & 0xFFFFFFFF
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & 0xFFFFFFFF
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & 0xFFFFFFFF
+        x ^= x >> 16
+        return x
+
+    e = np.asarray(e, dtype=np.uint64)
+    s = mix32(np.uint64((seed & 0xFFFFFFFF) ^ 0x9E3779B9)) ^ np.uint64(seed >> 32)
+    h = mix32((e & np.uint64(0xFFFFFFFF)) ^ mix32((e >> np.uint64(32)) ^ s))
+    return (h >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0) >= np.float32(p)
+
+
+def _tail_fwd_abi(hB, M, D, p, seed, offset_val=1.0):
+    """gnn_sage_norm_fwd_f32 on hB (M x D, D2 = 0) with scale 1 and a constant offset, so every
+    kept output is nonzero: returns Y."""
+    from gnn_amd import _lib
+
+    dev = hB.device
+    scale = torch.ones(D, device=dev)
+    offset = torch.full((D,), offset_val, device=dev)
+    Y = torch.empty(M, D, device=dev)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    _lib.check(_lib.lib().gnn_sage_norm_fwd_f32(hB.data_ptr(), D, D, None, 0, 0, None, None, scale.data_ptr(),
+                                                offset.data_ptr(), M, p, seed, 1, Y.data_ptr(), D,
+                                                mean.data_ptr(), rstd.data_ptr(), _lib.stream_of(dev)),
+               "gnn_sage_norm_fwd_f32")
+    torch.cuda.synchronize()
+    return Y
+
+
+@pytest.mark.parametrize("p,seed", [(0.1, 0x123456789ABCDEF), (0.5, 7), (0.3, (1 << 63) + 12345)])
+def test_dropout_mask_matches_hash_definition(dev, p, seed):
+    M, D = 777, 1000
+    hB = torch.randn(M, D, device=dev)
+    Y = _tail_fwd_abi(hB, M, D, p, seed, offset_val=50.0)  # |normalised| << 50: kept => nonzero
+    e = np.arange(M * D, dtype=np.uint64)
+    ref = _keep_mask_ref(seed, e, p).reshape(M, D)
+    assert np.array_equal((Y != 0).cpu().numpy(), ref)
+
+
+def test_dropout_mask_past_2_32_elements(dev):
+    """M * D >= 2^32 (the per-float4 hi32 path): the row holding element 2^32 straddles the
+    boundary (D = 1000); its mask and its neighbours' match the definition."""
+    D = 1000
+    M = (1 << 32) // D + 3
+    free, _ = torch.cuda.mem_get_info()
+    if free < 2 * M * D * 4 + (4 << 30):
+        pytest.skip("needs ~35 GB of free HBM")
+    hB = torch.ones(M, D, device=dev)  # every row constant: y = offset exactly where kept
+    Y = _tail_fwd_abi(hB, M, D, 0.25, 99, offset_val=1.0)
+    del hB
+    r0 = (1 << 32) // D - 1
+    rows = Y[r0:r0 + 4].cpu().numpy()
+    del Y
+    e = (np.arange(r0 * D, (r0 + 4) * D, dtype=np.uint64))
+    ref = _keep_mask_ref(99, e, 0.25).reshape(4, D)
+    assert np.array_equal(rows != 0, ref)
+    assert np.all(rows[ref] == np.float32(1.0) / np.float32(0.75))

@@ -55,3 +55,40 @@ def test_clip_to_flat_then_step(dev):
     torch.cuda.synchronize()
     for p, q in zip(ref, mine):
         torch.testing.assert_close(q.detach(), p.detach(), rtol=2e-6, atol=2e-7)
+
+
+def test_clip_adam_flat_views_unaligned(dev):
+    """Parameters and gradients as views of one flat buffer (the executor's layout): tensors
+    start at offsets that are not 16-byte aligned, so full chunks take the per-element path
+    and aligned ones the float4 path; both match torch."""
+    shapes = [(41,), (512, 602), (3,), (1024, 7), (9000,)]
+    sizes = [int(torch.Size(s).numel()) for s in shapes]
+    base = _params(dev, 5, [(sum(sizes),)])[0]
+    gbase = _params(dev, 6, [(sum(sizes),)])[0] / 10
+
+    def views(buf):
+        out, off = [], 0
+        for s, n in zip(shapes, sizes):
+            out.append(buf[off:off + n].view(*s))
+            off += n
+        return out
+
+    ref = [p.clone().requires_grad_(True) for p in views(base)]
+    flat = base.clone()
+    mine = [p.requires_grad_(True) for p in views(flat)]
+    gflat = gbase.clone()
+    for p, q, g in zip(ref, mine, views(gflat)):
+        p.grad = g.clone()
+        q.grad = g  # a view of gflat: unaligned where the offset is
+    opt_ref = torch.optim.Adam(ref, lr=0.01)
+    opt = ClipAdam(mine, lr=0.01, max_norm=5.0)
+    for _ in range(3):
+        torch.nn.utils.clip_grad_norm_(ref, 5.0)
+        opt_ref.step()
+        opt.step()
+        for p, g in zip(ref, views(gbase / 10)):
+            p.grad = g.clone()
+        gflat.copy_(gbase / 10)
+    torch.cuda.synchronize()
+    for p, q in zip(ref, mine):
+        torch.testing.assert_close(q.detach(), p.detach(), rtol=2e-6, atol=2e-7)
