@@ -15,7 +15,7 @@ What is pinned by executing the reference: LADIES sampling (RNG sequence, sub-gr
 normfact, sampled_nodes, placement masks), create_buffer placement maps, torch.sparse.mm
 SpMM outputs, and a GraphSAGE/GCN forward/backward/Adam step with the reference modules.
 
-Usage: python tests/golden/make_golden.py [--subgraph]   (writes tests/golden/*.npz)
+Usage: python tests/golden/make_golden.py [--subgraph | --spmm-wide]   (writes tests/golden/*.npz)
 """
 from __future__ import annotations
 
@@ -277,9 +277,40 @@ def subgraph_goldens():
     print("subgraph fixtures written to", HERE)
 
 
+WIDE_CASES = (("c2", (0, 1, 2)), ("c0", (2,)))  # (ladies_tiny case, layers) at the hidden width
+WIDE_F = 1024
+
+
+def spmm_wide_goldens():
+    """torch.sparse.mm forward / Aᵀ.coalesce() backward (the reference's CPU path,
+    custom_sparse_ops.py:25,36) at F = 1024, the GraphSAGE hidden width the layer-1/2
+    aggregations run at, on the reference sampler's sub-graphs already in ladies_tiny.npz
+    -> spmm_wide.npz. X and G are regenerated from the seed by the tests (only Y, dX stored)."""
+    z = np.load(os.path.join(HERE, "ladies_tiny.npz"))
+    out = {}
+    for case, layers in WIDE_CASES:
+        for li in layers:
+            shape = tuple(int(v) for v in z[f"{case}_adj{li}_shape"])
+            a = torch.sparse_coo_tensor(torch.from_numpy(z[f"{case}_adj{li}_indices"]),
+                                        torch.from_numpy(z[f"{case}_adj{li}_values"]), shape).coalesce()
+            g = torch.Generator().manual_seed(7000 + 100 * li + int(case[1:]))
+            X = torch.randn(shape[1], WIDE_F, generator=g)
+            G = torch.randn(shape[0], WIDE_F, generator=g)
+            Xr = X.clone().requires_grad_(True)
+            Y = _SpMM.apply(a, Xr)
+            Y.backward(G)
+            out[f"{case}_l{li}_Y"] = Y.detach().numpy()
+            out[f"{case}_l{li}_dX"] = Xr.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "spmm_wide.npz"), **out)
+    print("wide SpMM fixtures written to", HERE)
+
+
 if __name__ == "__main__":
     if "--subgraph" in sys.argv:
         subgraph_goldens()
+    elif "--spmm-wide" in sys.argv:
+        spmm_wide_goldens()
     else:
         main()
         subgraph_goldens()
+        spmm_wide_goldens()

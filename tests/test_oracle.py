@@ -44,6 +44,32 @@ def test_spmm_oracle_matches_torch_sparse_mm_golden(golden):
             np.testing.assert_allclose(O.spmm_f32(trp, trc, trv, G), s[f"l{li}_F{F}_dX"], rtol=1e-5, atol=1e-5)
 
 
+WIDE_CASES = (("c2", (0, 1, 2)), ("c0", (2,)))  # tests/golden/make_golden.py spmm_wide_goldens
+
+
+def wide_inputs(z, case, li, F=1024):
+    """X, G of one spmm_wide.npz entry, regenerated from the seed make_golden.py used."""
+    shape = tuple(int(v) for v in z[f"{case}_adj{li}_shape"])
+    g = torch.Generator().manual_seed(7000 + 100 * li + int(case[1:]))
+    return shape, torch.randn(shape[1], F, generator=g), torch.randn(shape[0], F, generator=g)
+
+
+def test_spmm_oracle_matches_wide_golden(golden):
+    """F = 1024 (the hidden width of the layer-1/2 aggregations): the oracle's fp32 chain and
+    its canonical transpose against the reference CPU path's outputs (spmm_wide.npz)."""
+    z = golden("ladies_tiny.npz")
+    s = golden("spmm_wide.npz")
+    for case, layers in WIDE_CASES:
+        for li in layers:
+            shape, X, G = wide_inputs(z, case, li)
+            rowptr, col, val = _coo_to_csr(z[f"{case}_adj{li}_indices"], z[f"{case}_adj{li}_values"], shape)
+            trp, trc, trv = O.csr_transpose(rowptr, col, val, int(shape[1]))
+            np.testing.assert_allclose(O.spmm_f32(rowptr, col, val, X.numpy()), s[f"{case}_l{li}_Y"],
+                                       rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(O.spmm_f32(trp, trc, trv, G.numpy()), s[f"{case}_l{li}_dX"],
+                                       rtol=1e-5, atol=1e-5)
+
+
 def test_transpose_matches_torch_coalesce():
     rng = np.random.default_rng(0)
     M, K = 300, 200

@@ -399,6 +399,26 @@ def test_reference_golden_spmm(dev, golden):
             np.testing.assert_allclose(Xd.grad.cpu().numpy(), s[f"l{li}_F{F}_dX"], rtol=RTOL, atol=ATOL)
 
 
+def test_reference_golden_spmm_wide(dev, golden):
+    """F = 1024, the hidden width of the layer-1/2 aggregations: forward and backward against
+    the reference CPU path's outputs (spmm_wide.npz; X, G regenerated from make_golden's seeds)."""
+    z = golden("ladies_tiny.npz")
+    s = golden("spmm_wide.npz")
+    for case, layers in (("c2", (0, 1, 2)), ("c0", (2,))):
+        for li in layers:
+            shape = tuple(int(v) for v in z[f"{case}_adj{li}_shape"])
+            g = torch.Generator().manual_seed(7000 + 100 * li + int(case[1:]))
+            X = torch.randn(shape[1], 1024, generator=g)
+            G = torch.randn(shape[0], 1024, generator=g)
+            A = torch.sparse_coo_tensor(torch.from_numpy(z[f"{case}_adj{li}_indices"]),
+                                        torch.from_numpy(z[f"{case}_adj{li}_values"]), shape).coalesce().to(dev)
+            Xd = X.to(dev).requires_grad_(True)
+            Y = cso.spmm(A, Xd)
+            Y.backward(G.to(dev))
+            np.testing.assert_allclose(Y.detach().cpu().numpy(), s[f"{case}_l{li}_Y"], rtol=RTOL, atol=ATOL)
+            np.testing.assert_allclose(Xd.grad.cpu().numpy(), s[f"{case}_l{li}_dX"], rtol=RTOL, atol=ATOL)
+
+
 def test_reference_golden_operand(dev, golden):
     """create_coo_tensor on the exact inputs the reference sampler produced (int16 colidx)."""
     z = golden("ladies_tiny.npz")
