@@ -522,19 +522,34 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
   if (cs >= nnz) return;
   const int ce = min(cs + 256, nnz);
   const int rf = wave_first_true(0, nrows, lane, [&](int r) { return rowptr[r + 1] > cs; });
-  const int rl = wave_first_true(rf, nrows, lane, [&](int r) { return rowptr[r + 1] >= ce; });
+  // The ends of rows rf, rf+1, ... one per lane; entry i is in row rf + #{ends <= i}. When
+  // fewer than 64 row ends fall inside the chunk that count is a uniform loop over them
+  // (no per-entry search of rowptr in global memory).
+  const int e = (rf + 1 + lane <= nrows) ? rowptr[rf + 1 + lane] : INT_MAX;
+  const int nin = __popcll(__ballot(e < ce));
+  int rl = rf;
+  if (nin == 64) rl = wave_first_true(rf, nrows, lane, [&](int r) { return rowptr[r + 1] >= ce; });
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int i = cs + t * 64 + lane;
+    int k = 0;
+    if (nin < 64) {
+      for (int j = 0; j < nin; ++j) k += (i >= __builtin_amdgcn_readlane(e, j)) ? 1 : 0;
+    }
+    const int rend = __shfl(e, k < 64 ? k : 63);
     if (i < ce) {
-      int lo = rf, hi = rl;  // the largest r with rowptr[r] <= i is the row holding i
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (rowptr[mid] <= i) lo = mid; else hi = mid - 1;
+      int lo = rf + k, end = rend;
+      if (nin == 64) {  // the largest r with rowptr[r] <= i is the row holding i
+        int hi = rl;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (rowptr[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        end = rowptr[lo + 1];
       }
       const int c = (int)colidx[i];
-      if (i + 1 < rowptr[lo + 1]) bad |= c > (int)colidx[i + 1];
+      if (i + 1 < end) bad |= c > (int)colidx[i + 1];
       const double inv = 1.0 / (double)(fullrowptr[lo + 1] - fullrowptr[lo]);
       out_col[i] = c;
       out_val[i] = (float)(inv * (double)normfact[c]);
@@ -555,17 +570,26 @@ __global__ __launch_bounds__(256) void build_operand_t_kernel(
   if (cs >= nnz) return;
   const int ce = min(cs + 256, nnz);
   const int cf = wave_first_true(0, ncols, lane, [&](int c) { return colptr[c + 1] > cs; });
-  const int cl = wave_first_true(cf, ncols, lane, [&](int c) { return colptr[c + 1] >= ce; });
+  // column ends one per lane, as in build_operand_flat_kernel
+  const int e = (cf + 1 + lane <= ncols) ? colptr[cf + 1 + lane] : INT_MAX;
+  const int nin = __popcll(__ballot(e < ce));
+  int cl = cf;
+  if (nin == 64) cl = wave_first_true(cf, ncols, lane, [&](int c) { return colptr[c + 1] >= ce; });
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int i = cs + t * 64 + lane;
     if (i < ce) {
-      int lo = cf, hi = cl;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (colptr[mid] <= i) lo = mid; else hi = mid - 1;
-      }
       const int r = rows[i];
+      int lo = cf;
+      if (nin < 64) {
+        for (int j = 0; j < nin; ++j) lo += (i >= __builtin_amdgcn_readlane(e, j)) ? 1 : 0;
+      } else {
+        int hi = cl;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (colptr[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+      }
       const double inv = 1.0 / (double)(fullrowptr[r + 1] - fullrowptr[r]);
       out_val[i] = (float)(inv * (double)normfact[lo]);
     }
