@@ -507,6 +507,12 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
     build_operand_row<CT>(fullrowptr, rowptr, colidx, normfact, r, out_col, out_val, sk[w], sv[w], lane);
 }
 
+// nonzeros per wave in the flat operand builders (a multiple of 64)
+#ifndef GNN_BUILD_CHUNK
+#define GNN_BUILD_CHUNK 64
+#endif
+constexpr int BUILD_CHUNK = GNN_BUILD_CHUNK;
+
 // Flat build: a wave per 256 consecutive nonzeros (nnz-balanced, ~4 loads in flight per
 // lane), each lane finding its row by a short binary search between the chunk's first and
 // last rows. Writes col/val for every entry and raises `flag` to `gen` if any row is out of
@@ -518,9 +524,9 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
     int* __restrict__ out_col, float* __restrict__ out_val,
     unsigned long long* __restrict__ flag, unsigned long long gen) {
   const int lane = threadIdx.x & 63;
-  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 256;
+  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * BUILD_CHUNK;
   if (cs >= nnz) return;
-  const int ce = min(cs + 256, nnz);
+  const int ce = min(cs + BUILD_CHUNK, nnz);
   const int rf = wave_first_true(0, nrows, lane, [&](int r) { return rowptr[r + 1] > cs; });
   // The ends of rows rf, rf+1, ... one per lane; entry i is in row rf + #{ends <= i}. When
   // fewer than 64 row ends fall inside the chunk that count is a uniform loop over them
@@ -531,7 +537,7 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
   if (nin == 64) rl = wave_first_true(rf, nrows, lane, [&](int r) { return rowptr[r + 1] >= ce; });
   bool bad = false;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < BUILD_CHUNK / 64; ++t) {
     const int i = cs + t * 64 + lane;
     int k = 0;
     if (nin < 64) {
@@ -566,9 +572,9 @@ __global__ __launch_bounds__(256) void build_operand_t_kernel(
     const int* __restrict__ fullrowptr, const int* __restrict__ colptr, const int* __restrict__ rows,
     const float* __restrict__ normfact, int ncols, int nnz, float* __restrict__ out_val) {
   const int lane = threadIdx.x & 63;
-  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 256;
+  const int cs = (blockIdx.x * 4 + (threadIdx.x >> 6)) * BUILD_CHUNK;
   if (cs >= nnz) return;
-  const int ce = min(cs + 256, nnz);
+  const int ce = min(cs + BUILD_CHUNK, nnz);
   const int cf = wave_first_true(0, ncols, lane, [&](int c) { return colptr[c + 1] > cs; });
   // column ends one per lane, as in build_operand_flat_kernel
   const int e = (cf + 1 + lane <= ncols) ? colptr[cf + 1 + lane] : INT_MAX;
@@ -576,7 +582,7 @@ __global__ __launch_bounds__(256) void build_operand_t_kernel(
   int cl = cf;
   if (nin == 64) cl = wave_first_true(cf, ncols, lane, [&](int c) { return colptr[c + 1] >= ce; });
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < BUILD_CHUNK / 64; ++t) {
     const int i = cs + t * 64 + lane;
     if (i < ce) {
       const int r = rows[i];
@@ -1438,7 +1444,7 @@ int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* 
   const bool sorted = flag == nullptr;
   const unsigned long long gen = 1;
   if (!sorted) GNN_HIP(hipMemsetAsync(flag, 0, sizeof(*flag), st), "operand flag memset");
-  const dim3 gflat((unsigned)ceil_div(nnz, 1024));  // 4 waves x 256 nonzeros
+  const dim3 gflat((unsigned)ceil_div(nnz, 4 * BUILD_CHUNK));  // 4 waves x BUILD_CHUNK nonzeros
   const dim3 gfix(16);  // usually a no-op (gated): keep the launch small
   switch (colidx_bytes) {
     case 2:
@@ -1484,7 +1490,7 @@ int gnn_build_operand_t_f32(const int32_t* fullrowptr, const int32_t* colptr, co
   GNN_REQUIRE(nrows < INT_MAX && ncols < INT_MAX && nnz < INT_MAX, "gnn_build_operand_t_f32: sizes must be < 2^31");
   if (ncols == 0 || nnz == 0) return 0;
   GNN_REQUIRE(fullrowptr && colptr && rows && normfact && val_t, "gnn_build_operand_t_f32: NULL input");
-  build_operand_t_kernel<<<dim3((unsigned)ceil_div(nnz, 1024)), dim3(256), 0, (hipStream_t)stream>>>(
+  build_operand_t_kernel<<<dim3((unsigned)ceil_div(nnz, 4 * BUILD_CHUNK)), dim3(256), 0, (hipStream_t)stream>>>(
       fullrowptr, colptr, rows, normfact, (int)ncols, (int)nnz, val_t);
   GNN_LAUNCHED("build_operand_t_kernel");
   return 0;
