@@ -585,6 +585,10 @@ def main():
         gsteps = max(1, min(args.steps, args.gpu_step_batches))
         pre = [next(it) for _ in range(nwarm + gsteps)]
         loader.close()
+        if exchange is not None:
+            # the look-ahead negotiations finish before the passes below re-negotiate these plans on
+            # this thread (Stager.issue): never two threads' collectives on the metadata group
+            it.close()
         native = not args.python_loader
         if native:
             # the batch blobs (CSR pieces or GPU-extraction inputs, labels, index arrays, host
@@ -619,9 +623,13 @@ def main():
             cso.enable_timing(False)
             recs = cso.take_timing_records()
             k_[0] = nwarm
-            if native:  # the second pass rebuilds the device batches
-                for j in range(len(dbs)):
-                    dbs[j] = None
+        if native:
+            # every pass uploads each blob afresh: drop the device copies the warm-up / events pass
+            # left on the batches (device_blob caches one), so the H2D is inside this timing too
+            torch.cuda.synchronize()
+            for j in range(len(dbs)):
+                dbs[j] = None
+                pre[j].host.drop_device()
         stager.timing = []
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
         h_bytes, h_sec = stager.take_timing()
@@ -659,7 +667,11 @@ def main():
                 st.sort_stats("cumulative").print_stats(45)
     else:
         loader.close()
+        if exchange is not None:
+            it.close()
     final_loss = float(loss.item()) if loss is not None else float("nan")
+    if dx:  # every GPU extraction of the run agreed with the host's counts (syncs; outside the timings)
+        sampler.device_graph(loader.graph, dev).check()
 
     cpu = None
     sampler_cost = None

@@ -102,6 +102,7 @@ _SAMPLER_SIGNATURES = {
                                    ctypes.POINTER(_VP)]),
     "gnn_fastgcn_sample": (_INT, [_VP, _VP, _VP, _I64, _VP, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                   ctypes.POINTER(_VP)]),
+    "gnn_fastgcn_p_changed": (None, []),
     "gnn_ladies_layer_dims": (_INT, [_VP, ctypes.c_int32, ctypes.POINTER(_I64)]),
     "gnn_ladies_layer_copy": (_INT, [_VP, ctypes.c_int32, _VP, _VP, _VP, _VP, _VP]),
     "gnn_ladies_layer_csc": (_INT, [_VP, ctypes.c_int32, _VP, _VP]),

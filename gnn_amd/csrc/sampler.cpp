@@ -208,6 +208,9 @@ struct Graph {
 // per sampler thread, reused across calls (acquire): fresh multi-MB allocations are served
 // by mmap and pay a page fault per 4 KB on first touch — the layer extraction's scratch
 // alone (up to 23 MB per layer) cost ~40 % of a Reddit batch before it was reused.
+// Bumped by gnn_fastgcn_p_changed(): invalidates every thread's FastGCN candidate cache.
+std::atomic<uint64_t> g_fastgcn_generation{0};
+
 class Work {
  public:
   explicit Work(const Graph& g) : g_(g), cnt(g.N, 0), bits((g.N + 63) / 64), wrank((g.N + 63) / 64),
@@ -424,7 +427,9 @@ class Work {
 
   // FastGCN: choice over the nodes with p > 0 (NaN p never live), layer-independent: the
   // candidate list, their p and the untouched cdf are kept per thread for the p array they
-  // came from (identified by its address, length and 64 sampled values).
+  // came from (identified by its address, length, 64 sampled values and the process-wide
+  // generation that gnn_fastgcn_p_changed() bumps: a caller that rewrites p in place, or frees
+  // it and allocates another, announces it there, so no stale candidate list is reused).
   void choose_by_p(MT19937& rng, const double* p, int64_t s_num) {
     const size_t N = g_.N;
     uint64_t sig = 1469598103934665603ull;
@@ -433,7 +438,8 @@ class Work {
       std::memcpy(&b, &p[(k * (N - 1)) / 63], 8);
       sig = (sig ^ b) * 1099511628211ull;
     }
-    if (fg_p != p || fg_n != N || fg_sig != sig) {
+    const uint64_t gen = g_fastgcn_generation.load(std::memory_order_acquire);
+    if (fg_p != p || fg_n != N || fg_sig != sig || fg_gen != gen) {
       fg_live.clear();
       fg_pv.clear();
       for (size_t v = 0; v < N; ++v) {
@@ -451,6 +457,7 @@ class Work {
       fg_p = p;
       fg_n = N;
       fg_sig = sig;
+      fg_gen = gen;
     }
     choice_without_replacement(rng, fg_live.data(), fg_pv.data(), false, fg_base.data(), fg_live.size(),
                                std::min<int64_t>((int64_t)fg_live.size(), s_num), taken, found, cdf_work, xs, js);
@@ -589,6 +596,7 @@ class Work {
   const double* fg_p = nullptr;
   size_t fg_n = 0;
   uint64_t fg_sig = 0;
+  uint64_t fg_gen = ~0ull;
   bool clean_ = true;
 };
 
@@ -814,6 +822,8 @@ int gnn_subgraph_sample(const int64_t* indptr, const int32_t* indices, const flo
     return fail("gnn_subgraph_sample: out of host memory");
   }
 }
+
+void gnn_fastgcn_p_changed(void) { g_fastgcn_generation.fetch_add(1, std::memory_order_acq_rel); }
 
 int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const float* data, int64_t num_nodes,
                        const double* p, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,

@@ -161,13 +161,22 @@ _I32, _I64, _F32 = np.dtype(np.int32), np.dtype(np.int64), np.dtype(np.float32)
 _TDT = {_I32: torch.int32, _I64: torch.int64, _F32: torch.float32}
 
 
+def _release_blob(release, handle, uploads) -> None:
+    """weakref.finalize of a NativeBatch: wait for the blob's uploads, then return it to the pool."""
+    for ev in uploads:
+        ev.synchronize()
+    uploads.clear()
+    release(handle)
+
+
 class NativeBatch:
     """One batch of the native loader: the host blob, its descriptor and views of its sections.
 
     Duck-types the parts of ``sampler.HostBatch`` the training pipeline and the benchmark read
     (``layers``, ``sampled_nodes``, ``input_nodes``, ``labels``, ``nnz()``, ``to_device``) and
     carries the X0 staging plan (``plan``). The blob goes back to the loader's pool when this
-    object dies — after the step that read it (the staging path keeps it alive until then)."""
+    object dies, and not before its uploads (``device_blob``) have completed: the device side
+    only reads the uploaded copy, so dropping the host batch early is safe."""
 
     def __init__(self, handle: int, store: Optional[staging.FeatureStore]):
         import weakref
@@ -180,7 +189,11 @@ class NativeBatch:
         self.desc = np.ctypeslib.as_array(dp, shape=(n.value,)).copy()
         self.nbytes = int(self.desc[H_BYTES])
         self.ptr = int(L.gnn_batch_blob(handle))
-        self._release = weakref.finalize(self, L.gnn_batch_release, handle)
+        # the pinned blob goes back to the loader's pool (where a worker may refill it at once)
+        # only after every upload that read it has completed: device_blob() records an event
+        # after its H2D into this holder, and the release waits for it
+        self._uploads = []
+        self._release = weakref.finalize(self, _release_blob, L.gnn_batch_release, handle, self._uploads)
         self.blob = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
         self.num_layers = int(self.desc[H_LAYERS])
         self.world = int(self.desc[H_WORLD])
@@ -264,8 +277,17 @@ class NativeBatch:
                 d = torch.empty(self.nbytes, dtype=torch.uint8, device=dev)
                 _lib.check(_lib.lib().gnn_memcpy_h2d_async(d.data_ptr(), self.ptr, self.nbytes, _lib.stream_of(dev)),
                            "gnn_memcpy_h2d_async")
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+            # completed uploads need no wait at release time: keep the list short
+            self._uploads[:] = [e for e in self._uploads if not e.query()] + [ev]
             self._dev = (dev, d)
         return self._dev[1]
+
+    def drop_device(self) -> None:
+        """Forget the uploaded copy: the next device_blob() uploads the blob again (the
+        benchmark's second pass over pre-sampled batches times a real H2D per batch)."""
+        self._dev = None
 
     def _d(self, slot: int, dt: np.dtype) -> torch.Tensor:
         off, cnt = int(self.desc[slot]), int(self.desc[slot + 1])

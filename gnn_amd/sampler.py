@@ -212,6 +212,8 @@ class DeviceGraph:
 
     def __init__(self, graph: "NativeGraph", device):
         dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())  # where a bare 'cuda' allocates
         self.device = dev
         self.num_nodes = graph.num_nodes
         self.indptr = torch.from_numpy(graph.indptr).to(dev)
@@ -290,7 +292,13 @@ class NativeGraph:
     @property
     def fastgcn_p(self) -> np.ndarray:
         if self._fastgcn_p is None:
-            self._fastgcn_p = fastgcn_probability(self.lap)
+            from . import _lib
+
+            p = fastgcn_probability(self.lap)
+            p.flags.writeable = False  # the native draw caches per-p state: no in-place edits
+            # a fresh array may reuse a freed one's address: drop every thread's cached candidates
+            _lib.sampler_lib().gnn_fastgcn_p_changed()
+            self._fastgcn_p = p
         return self._fastgcn_p
 
 
@@ -322,9 +330,10 @@ def colcount_api(graph, device) -> "_ColCountApi":
     dg = device_graph(graph, device)
     L = _lib.lib()
     fp = lambda f: ctypes.cast(f, ctypes.c_void_p).value
+    # the device that holds the graph's arrays (device_graph resolves a bare 'cuda' the same way)
+    index = dg.device.index if dg.device.index is not None else torch.cuda.current_device()
     api = _ColCountApi(fp(L.gnn_colcount_create), fp(L.gnn_colcount_add), fp(L.gnn_colcount_reset),
-                       fp(L.gnn_colcount_destroy), dg.device.index if dg.device.index is not None else 0,
-                       dg.indptr.data_ptr(), dg.indices.data_ptr())
+                       fp(L.gnn_colcount_destroy), index, dg.indptr.data_ptr(), dg.indices.data_ptr())
     api._dg = dg  # the device arrays stay alive with the struct
     return api
 

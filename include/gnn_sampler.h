@@ -98,6 +98,12 @@ int gnn_fastgcn_sample(const int64_t* indptr, const int32_t* indices, const floa
                        const double* p, const int64_t* batch_nodes, int64_t batch_size, const int64_t* samp_num,
                        const int32_t* orders, int32_t num_layers, uint32_t seed, gnn_ladies_result** out);
 
+/* The FastGCN draw keeps, per sampler thread, the candidate list and base cdf of the p array it
+ * last saw (keyed by its address, length and a sample of its values). A caller that rewrites a
+ * p array in place — or frees one and passes another that may reuse the address — calls this
+ * first: every thread rebuilds its cache on its next draw. Thread-safe. */
+void gnn_fastgcn_p_changed(void);
+
 /* dims of layer `layer` (bottom-up, as the returned adjs): {M, K, nnz, n_sampled, s_num}.
  * Returns 1 if the layer has order 0 (no sub-graph), 0 otherwise. */
 int gnn_ladies_layer_dims(const gnn_ladies_result* r, int32_t layer, int64_t dims[5]);

@@ -92,6 +92,125 @@ def _trainer_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
+NSPEC = dict(name="dist-native", num_nodes=6000, num_edge_samples=40_000, num_feats=100, num_classes=41,
+             train_frac=0.5, valid_frac=0.1)
+NSAMP, NBS = 700, 64
+
+
+def _native_batch(rank, device_extract):
+    """Rank `rank`'s batch of the native-executor case: LADIES with the lower layers extracted on
+    the GPU (device_extract=True: CsrOperands + transposes + row maps, what the bench feeds the
+    executor) or on the host (the CPU reference's operands; the draw is identical)."""
+    from gnn_amd import graphs, sampler
+
+    spec = graphs.GraphSpec(*NSPEC.values())
+    A, labels, feats, ncls, train, *_ = graphs.make_dataset(spec, seed=3)
+    lap = graphs.lap_matrix(A, "graphsage")
+    N = A.shape[0]
+    chunk = sampler.rank_batches(train, NBS, rank, 2, 1)[0]
+    hb = sampler.ladies_sample_host(50 + rank, chunk, np.array([NSAMP] * 5), N, lap, labels, [1, 1, 1],
+                                    np.full(N, -1, np.int64), np.zeros(N, np.int64), None, 1.0, [0],
+                                    device_extract=device_extract)
+    return hb, feats, ncls
+
+
+def _native_model(seed, F, ncls, fused):
+    from gnn_amd.models import build_model
+
+    torch.manual_seed(seed)
+    return build_model("graphsage", F, 32, [1, 1, 1], ncls, dropout=0.0, fused=fused)
+
+
+def _native_trainer_worker(rank, world, port, q):
+    """The benchmark's N > 1 branch: executor step -> ClipAdam.clip_to_flat -> all_reduce(SUM) ->
+    step(clipped=True) (train.py, Trainer.step with the executor)."""
+    _env(rank, world, port)
+    import torch.distributed as dist
+
+    try:
+        from gnn_amd import staging
+        from gnn_amd.train import Trainer, init_distributed
+
+        init_distributed()
+        dev = torch.device("cuda", 0)
+        hb, feats, ncls = _native_batch(rank, True)
+        F = feats.shape[1]
+        net = _native_model(200 + rank, F, ncls, True).to(dev)  # rank-specific init: the broadcast fixes it
+        tr = Trainer(net, LR, dev)
+        db = hb.to_device(dev, with_coo=False)
+        x = torch.zeros((hb.num_input_nodes, staging.padded_ld(F)), dtype=torch.float32)
+        x[:, :F] = feats[torch.from_numpy(np.asarray(hb.input_nodes, np.int64))]
+        x0 = x.to(dev)[:, :F]
+        assert tr.executor is not None and tr.executor.supports(x0, db.adjs, db.sampled_nodes, db.labels), \
+            "the executor branch must be the one exercised"
+        losses = [float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels)) for _ in range(2)]
+        torch.cuda.synchronize()
+        q.put((rank, "ok", losses, [p.detach().cpu().numpy().copy() for p in net.parameters()]))
+    except Exception as e:
+        q.put((rank, f"error: {e!r}", None, None))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _native_reference_two_steps():
+    """main.py:146-170 on the CPU for the native case: per-rank grads of the host-extracted
+    batches through the CPU branch (torch.sparse.mm), per-rank clip_grad_norm_(5), SUM, Adam."""
+    from gnn_amd.models import loss as loss_fn
+
+    batches = [_native_batch(r, False) for r in range(2)]
+    F, ncls = batches[0][1].shape[1], batches[0][2]
+    nets = [_native_model(200, F, ncls, False) for _ in range(2)]  # rank 0's init on both
+    params = list(nets[0].parameters())
+    opt = torch.optim.Adam(params, lr=LR)
+    inputs = [hb.cpu_inputs(feats) for hb, feats, _ in batches]
+    sums, losses = [], []
+    for _ in range(2):
+        with torch.no_grad():
+            for p0, p1 in zip(nets[0].parameters(), nets[1].parameters()):
+                p1.copy_(p0)
+        grads = []
+        for r in range(2):
+            net = nets[r]
+            net.zero_grad()
+            adjs, x0, sampled, y = inputs[r]
+            lo = loss_fn(net(x0, adjs, sampled), y, True, "cpu")
+            lo.backward()
+            losses.append(float(lo.detach()))
+            torch.nn.utils.clip_grad_norm_(net.parameters(), 5)
+            grads.append([p.grad.detach().clone() for p in net.parameters()])
+        total = [a + b for a, b in zip(*grads)]
+        for p, g in zip(params, total):
+            p.grad = g
+        sums.append(total)
+        opt.step()
+    return [p.detach().numpy() for p in params], sums, losses
+
+
+def test_trainer_executor_dp_step_matches_reference():
+    """The branch bench.py runs at N > 1 (executor + flat clip + all_reduce + Adam on views),
+    with GPU-extracted CsrOperands as the bench feeds them, against main.py:146-170 semantics."""
+    out = _spawn(_native_trainer_worker)
+    for rank, status, _, _ in out:
+        assert status == "ok", f"rank {rank}: {status}"
+    ref, sums, ref_losses = _native_reference_two_steps()
+    for rank in range(2):
+        for s in range(2):
+            got, want = out[rank][2][s], ref_losses[2 * s + rank]
+            assert abs(got - want) <= 1e-4 * abs(want) + 1e-6, (rank, s, got, want)
+    p0, p1 = out[0][3], out[1][3]
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b), "ranks disagree after the summed update"
+    for i, (got, want) in enumerate(zip(p0, ref)):
+        sure = np.ones(got.shape, bool)
+        for s in sums:
+            gg = s[i].numpy()
+            sure &= np.abs(gg) > 1e-4 * max(np.abs(gg).max(), 1e-12)
+        assert sure.mean() > 0.5
+        np.testing.assert_allclose(got[sure], want[sure], rtol=1e-4, atol=1e-6, err_msg=f"param {i}")
+
+
 def _exchange_worker(rank, world, port, q):
     _env(rank, world, port)
     import torch.distributed as dist

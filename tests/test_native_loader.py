@@ -137,3 +137,34 @@ def test_native_batch_on_device(dev, dx):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.gpu
+def test_blob_dropped_right_after_upload(dev):
+    """A NativeBatch dropped while its upload is still queued: the pinned blob must not go back
+    to the loader's pool (where a worker refills it for the next batch) before the H2D has read
+    it. The upload is held behind a GPU spin on its stream, the batch is dropped at once, and the
+    workers keep producing; the device copy must equal the blob as it was at upload time."""
+    import gc
+
+    lap, labels, feats, train, pl = _setup()
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    b = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], store=store, workers=3, seed=4, prefetch=2)
+    side = torch.cuda.Stream(dev)
+    try:
+        it = b.epoch(1)
+        for _ in range(6):
+            lb = next(it)
+            want = torch.from_numpy(lb.host.blob.copy())
+            with torch.cuda.stream(side):
+                torch.cuda._sleep(20_000_000)  # the H2D below waits behind this spin
+                d = lb.host.device_blob(dev)
+            del lb  # the blob's finaliser runs here
+            gc.collect()
+            next_lb = next(it)  # workers refill pooled blobs meanwhile
+            torch.cuda.synchronize()
+            assert torch.equal(d.cpu(), want), "the uploaded blob was overwritten before its copy ran"
+            del next_lb
+    finally:
+        b.close()

@@ -209,6 +209,35 @@ def test_fastgcn_sampling_law():
     assert abs(hits[mid].sum() / expect.sum() - 1) < 0.1
 
 
+def test_fastgcn_cache_invalidated_by_p_changed():
+    """The native FastGCN draw caches the candidate list of the p array it last saw per thread;
+    an in-place rewrite of p announced through gnn_fastgcn_p_changed() must not reuse it: the
+    next draw equals the numpy restatement on the rewritten p."""
+    N = 2000
+    lap = _lap(N, 10, 21)
+    g = sampler.native_graph(lap)
+    p = np.array(g.fastgcn_p, copy=True)  # a writable array the test owns
+    assert not g.fastgcn_p.flags.writeable
+    g._fastgcn_p = p
+    args = (5, np.arange(16), np.array([60] * 2), N, lap, _labels(N), [1, 1], np.full(N, -1),
+            np.zeros(N, np.int64), None, 1.0, [0])
+    with ThreadPoolExecutor(1) as pool:  # one thread: its cache sees both calls
+        a = pool.submit(sampler.fastgcn_sample_host, *args).result()
+        # rewrite p in place: same address and length, and the 64 values the cache key samples
+        # ((k * (N - 1)) // 63) untouched — only the generation tells the change apart
+        keyed = np.zeros(N, bool)
+        keyed[(np.arange(64) * (N - 1)) // 63] = True
+        free = np.flatnonzero(~keyed)
+        p[free] = np.roll(p[free], 997)
+        _lib.sampler_lib().gnn_fastgcn_p_changed()
+        b = pool.submit(sampler.fastgcn_sample_host, *args).result()
+    ref = sampler.fastgcn_sample_host(*args, native=False)
+    assert np.array_equal(b.input_nodes, ref.input_nodes)
+    assert not np.array_equal(a.input_nodes, b.input_nodes)
+    for x, y in zip(b.layers, ref.layers):
+        assert np.array_equal(x.colidx, y.colidx) and np.array_equal(x.normfact, y.normfact)
+
+
 def test_native_errors():
     L = _lib.sampler_lib()
     h = ctypes.c_void_p()
