@@ -68,13 +68,13 @@ _SIGNATURES = {
     "gnn_head_bce_bwd_f32": (_INT, [_VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _VP, ctypes.c_float,
                                     ctypes.c_uint64, _INT, _VP, _VP, _VP, _VP, _I64, _VP]),
     # include/gnn_extract.h
-    "gnn_ladies_extract_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int32]),
+    "gnn_ladies_extract_workspace_bytes": (_SZ, [_I64, _I64, _I64, ctypes.c_int32, _I64, _I64]),
     "gnn_colcount_create": (_INT, [ctypes.c_int32, _I64, _VP, _VP, ctypes.POINTER(_VP)]),
     "gnn_colcount_add": (_INT, [_VP, _VP, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_VP), ctypes.POINTER(_VP)]),
     "gnn_colcount_reset": (_INT, [_VP]),
     "gnn_colcount_destroy": (None, [_VP]),
-    "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP,
-                                      _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
+    "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64,
+                                      _I64, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
     # include/gnn_step.h
     "gnn_train_step_workspace_bytes": (_SZ, [_VP]),
     "gnn_train_step_f32": (_INT, [_VP, _VP, _SZ, _VP]),

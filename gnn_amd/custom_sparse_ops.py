@@ -359,14 +359,17 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
 
 def extract_operand(graph, rows: torch.Tensor, cols: torch.Tensor, normfact: torch.Tensor, nnz: int,
                     rowseg: torch.Tensor, colseg: Optional[torch.Tensor] = None,
-                    colptr: Optional[torch.Tensor] = None) -> CsrOperand:
+                    colptr: Optional[torch.Tensor] = None, rowseg_total: Optional[int] = None,
+                    colseg_total: Optional[int] = None) -> CsrOperand:
     """adj = lap[rows, :][:, cols] with create_coo_tensor's values, built on the GPU from the
     graph resident there (gnn_ladies_extract_f32; ``graph`` a sampler.DeviceGraph): the
     operand of a LADIES layer whose draw ran on the host (sampler.py:114-139). ``nnz`` is the
     host-known entry count (the column counts of U over cols); ``rowseg`` U's row pointer (M+1).
     With ``colseg`` (offsets of lapᵀ's rows of cols, K+1) and ``colptr`` (the CSC column
     pointer, K+1; rows must be unique and ascending) the transpose is built too and cached on
-    the operand — the canonical Aᵀ (A.t().coalesce())."""
+    the operand — the canonical Aᵀ (A.t().coalesce()). ``rowseg_total`` / ``colseg_total`` =
+    rowseg[M] / colseg[K] (the graph entries scanned per direction; they size the launch): pass
+    the host's values — if omitted they are read back from the device (a synchronisation)."""
     for name, t in (("rows", rows), ("cols", cols), ("rowseg", rowseg)):
         _require(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), f"{name} must be contiguous int32 CUDA")
     _require(normfact.is_cuda and normfact.dtype == torch.float32 and normfact.numel() == cols.numel(),
@@ -386,14 +389,20 @@ def extract_operand(graph, rows: torch.Tensor, cols: torch.Tensor, normfact: tor
                          f"{name} must be int32 CUDA with K + 1 entries")
             rows_t = torch.empty(nnz, dtype=torch.int32, device=dev)
             val_t = torch.empty(nnz, dtype=torch.float32, device=dev)
+        if rowseg_total is None:
+            rowseg_total = int(rowseg[M].item())
+        if colptr is not None and colseg_total is None:
+            colseg_total = int(colseg[K].item())
         L = _lib.lib()
-        wsb = L.gnn_ladies_extract_workspace_bytes(graph.num_nodes, M, K, int(colptr is not None))
+        wsb = L.gnn_ladies_extract_workspace_bytes(graph.num_nodes, M, K, int(colptr is not None),
+                                                   int(rowseg_total), int(colseg_total or 0))
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         st = _stream(dev)
         _lib.check(L.gnn_ladies_extract_f32(
-            _ptr(graph.indptr), _ptr(graph.indices), graph.num_nodes, _ptr(graph.indptr_t), _ptr(graph.indices_t),
+            _ptr(graph.indptr), _ptr(graph.indices), _ptr(graph.degree), graph.num_nodes, _ptr(graph.indptr_t),
+            _ptr(graph.indices_t),
             _ptr(rows), M, _ptr(cols), K, _ptr(normfact), nnz, _ptr(rowseg), _ptr(colseg), _ptr(colptr),
-            _ptr(rowptr), _ptr(col), _ptr(val), _ptr(rows_t), _ptr(val_t), ws.data_ptr(), wsb, _ptr(graph.err), st),
+            int(rowseg_total), int(colseg_total or 0), _ptr(rowptr), _ptr(col), _ptr(val), _ptr(rows_t), _ptr(val_t), ws.data_ptr(), wsb, _ptr(graph.err), st),
             "gnn_ladies_extract_f32")
     op = CsrOperand(rowptr, col, val, (M, K))
     if colptr is not None:

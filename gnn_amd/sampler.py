@@ -183,7 +183,10 @@ class DeviceBatch:
             if ci is None:  # left to the GPU extraction (rows / cols / column counts from the draw)
                 _require_graph(self.graph)
                 tr = li >= csc_from
-                op = cso.extract_operand(self.graph, rows, cols, nf, nnz, fr, cs if tr else None, cp if tr else None)
+                hl = self.host.layers[li]  # host views of the same offsets: their totals size the launch
+                op = cso.extract_operand(self.graph, rows, cols, nf, nnz, fr, cs if tr else None, cp if tr else None,
+                                         rowseg_total=int(hl.fullrowptr[-1]),
+                                         colseg_total=int(hl.colseg[-1]) if tr else None)
                 coo = op.to_torch_coo()._indices() if with_coo else None
             else:
                 op, coo = cso.build_operand(fr, rp, ci, nf, shape[0], shape[1], with_coo=with_coo,
@@ -207,8 +210,8 @@ def _require_graph(graph) -> None:
 
 class DeviceGraph:
     """A NativeGraph's structure resident in device memory for gnn_ladies_extract_f32: canonical
-    CSR of lap (int64 indptr, int32 indices) and of lapᵀ (the same arrays when the structure is
-    symmetric), and an error flag the extraction raises if a device count disagrees with the host's."""
+    CSR of lap (int64 indptr, int32 indices, int32 row degrees) and of lapᵀ (the same arrays when
+    the structure is symmetric), and an error flag the extraction raises if a device count disagrees with the host's."""
 
     def __init__(self, graph: "NativeGraph", device):
         dev = torch.device(device)
@@ -218,6 +221,8 @@ class DeviceGraph:
         self.num_nodes = graph.num_nodes
         self.indptr = torch.from_numpy(graph.indptr).to(dev)
         self.indices = torch.from_numpy(graph.indices).to(dev)
+        # row degrees as int32 (one 4-byte load per kept entry for the transposed values)
+        self.degree = torch.from_numpy(np.diff(graph.indptr).astype(np.int32)).to(dev)
         self.symmetric, ipt, ixt = graph.transpose_structure
         if self.symmetric:
             self.indptr_t, self.indices_t = self.indptr, self.indices

@@ -29,13 +29,15 @@ extern "C" {
  *
  * Graph (device): the lap matrix as canonical CSR (indptr int64[num_nodes+1], indices int32,
  * columns ascending per row, no duplicates); indptr_t / indices_t: the same for lap^T (may alias
- * indptr / indices when the structure is symmetric). deg(v) = indptr[v+1] - indptr[v].
+ * indptr / indices when the structure is symmetric). deg(v) = indptr[v+1] - indptr[v]; degree
+ * int32[num_nodes] holds it (required with the transpose: its values' row degrees).
  * rows  int32[M]: U's rows (node ids) in order; cols int32[K]: after_nodes, strictly ascending;
  * normfact fp32[K]; nnz = number of entries of U[:, cols] (the sum of U's column counts over cols).
  * rowseg int32[M+1] = U's row pointer (exclusive scan of deg(rows[i])); colseg int32[K+1] = the
  * exclusive scan of lapᵀ's row lengths of cols (transpose only) — both host-known (the draw).
- * workspace: gnn_ladies_extract_workspace_bytes(num_nodes, M, K, transpose) bytes (no state is
- * kept between calls: concurrent calls on different streams need different workspaces).
+ * workspace: gnn_ladies_extract_workspace_bytes(num_nodes, M, K, transpose, rowseg_total,
+ * colseg_total) bytes (8 bytes per graph entry scanned plus tables; no state is kept between
+ * calls: concurrent calls on different streams need different workspaces).
  * Outputs: rowptr int32[M+1], col int32[nnz] (positions into cols, ascending per row),
  * val fp32[nnz] = (float)((1.0 / deg(rows[i])) * (double)normfact[col]) — identical to
  * gnn_build_operand_f32 on the host-extracted pieces with fullrowptr = rowseg.
@@ -43,17 +45,24 @@ extern "C" {
  * val_t fp32[nnz] receive the canonical CSR of adj^T (rows ascending in each column) whose row
  * pointer is colptr_t, the host's CSC column pointer (its column counts; not read here) — what
  * gnn_csr_transpose / A.t().coalesce() would produce.
- * Work is balanced over entries, not rows (power-law rows): a fixed number of waves per
- * direction each take a contiguous range of the concatenated graph rows; membership of a node
- * in cols / rows is a bitmap + per-word rank table, staged in LDS when it fits.
+ * rowseg_total = rowseg[M] and colseg_total = colseg[K] (transpose only; ignored otherwise): the
+ * graph entries scanned per direction, host-known like the offsets (they size the launch).
+ * Work is balanced over entries, not rows (power-law rows): each direction's concatenated graph
+ * rows are cut into equal contiguous ranges, one per wave, and every entry is read ONCE (the
+ * kept entries of a range go to a gapped buffer, then to their place after a scan of the
+ * per-range counts); membership of a node in cols / rows is a bitmap + per-word rank table.
  * err_flag (device int32, optional): OR-ed with 1 / 2 if the kept entries of A / A^T do not add up
- * to nnz (the writes stay inside the outputs). */
-size_t gnn_ladies_extract_workspace_bytes(int64_t num_nodes, int64_t M, int64_t K, int32_t transpose);
-int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, int64_t num_nodes, const int64_t* indptr_t,
-                           const int32_t* indices_t, const int32_t* rows, int64_t M, const int32_t* cols, int64_t K,
+ * to nnz (or a segment total differs from the device offsets). The outputs then stay safe to
+ * read: writes stay below nnz, entries past the kept ones are zero-filled (column / row 0, value
+ * 0) and rowptr is clamped to nnz. */
+size_t gnn_ladies_extract_workspace_bytes(int64_t num_nodes, int64_t M, int64_t K, int32_t transpose,
+                                          int64_t rowseg_total, int64_t colseg_total);
+int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, const int32_t* degree, int64_t num_nodes,
+                           const int64_t* indptr_t, const int32_t* indices_t, const int32_t* rows, int64_t M, const int32_t* cols, int64_t K,
                            const float* normfact, int64_t nnz, const int32_t* rowseg, const int32_t* colseg,
-                           const int32_t* colptr_t, int32_t* rowptr, int32_t* col, float* val, int32_t* rows_t,
-                           float* val_t, void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream);
+                           const int32_t* colptr_t, int64_t rowseg_total, int64_t colseg_total, int32_t* rowptr,
+                           int32_t* col, float* val, int32_t* rows_t, float* val_t, void* workspace,
+                           size_t workspace_bytes, int32_t* err_flag, void* stream);
 
 /* U's column counts for the LADIES draw on the GPU (reference sampler.py:116-122,
  * pi = norm(U, ord=0, axis=0)), for a host sampler thread (gnn_sampler.h: gnn_colcount_api).

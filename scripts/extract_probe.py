@@ -25,7 +25,12 @@ def timed(fn, reps):
     return float(np.median([a.elapsed_time(b) for a, b in ts])) * 1e3
 
 
-VARIANTS = [v for v in os.environ.get("VARIANTS", "").split(";") if v]  # e.g. "GNN_LX_LDS=0,GNN_LX_XW=8192"
+VARIANTS = [v for v in os.environ.get("VARIANTS", "").split(";") if v]  # e.g. "GNN_LX_XW=16384"
+
+
+def _totals(L, tr):
+    """The host-known segment totals (as the training path passes them: no device read-back)."""
+    return dict(rowseg_total=int(L.fullrowptr[-1]), colseg_total=int(L.colseg[-1]) if tr else None)
 
 
 def main():
@@ -52,12 +57,15 @@ def main():
             os.environ[k] = v
         for li in (0, 1):
             fr, rp, ci, nf, shape, cp, cr, rows, cols, nnz, cs = dd.raw[li]
-            us = timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr), reps)
-            ust = timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr, cs, cp), reps)
+            L = hd.layers[li]
+            us = timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr, **_totals(L, False)), reps)
+            ust = timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr, cs, cp, **_totals(L, True)), reps)
             print(json.dumps({"variant": var, "layer": li, "extract_us": round(us, 1), "with_t_us": round(ust, 1)}),
                   flush=True)
         for kv in var.split(","):
             os.environ.pop(kv.split("=")[0], None)
+        torch.cuda.synchronize()
+        dg.err.zero_()  # GNN_LX_FLAGS variants produce wrong counts by design
     for li in range(3):
         r = dd.raw[li]
         L = hd.layers[li]
@@ -65,10 +73,11 @@ def main():
         if L.on_device:
             fr, rp, ci, nf, shape, cp, cr, rows, cols, nnz, cs = r
             row["U_entries"] = int((dg.indptr[rows.long() + 1] - dg.indptr[rows.long()]).sum())
-            row["extract_us"] = round(timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr), reps), 1)
-            if li >= 1:
-                row["extract_with_t_us"] = round(
-                    timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr, cs, cp), reps), 1)
+            row["T_entries"] = int(L.colseg[-1])
+            row["extract_us"] = round(timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr,
+                                                                        **_totals(L, False)), reps), 1)
+            row["extract_with_t_us"] = round(
+                timed(lambda: cso.extract_operand(dg, rows, cols, nf, nnz, fr, cs, cp, **_totals(L, True)), reps), 1)
         fr, rp, ci, nf, shape, cp, cr = db.raw[li][:7]
 
         def build():
@@ -77,8 +86,7 @@ def main():
                 cso.attach_transpose(op, fr, cp, cr, nf)
         row["host_path_build_us"] = round(timed(build, reps), 1)
         print(json.dumps(row), flush=True)
-    if not os.environ.get("GNN_LX_FLAGS"):
-        dg.check()
+    dg.check()
 
 
 if __name__ == "__main__":
