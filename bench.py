@@ -443,6 +443,47 @@ def roofline_from(recs, step_batches, args, traffic, steps):
     return roof, detail
 
 
+def gather_ceiling(op, kernel_name, dev, reps=20, K=4096):
+    """The dominant aggregation kernel's own access shape over a CACHE-RESIDENT table: the same
+    instantiation (VW, G, NJ forced), the same row lengths (the operand's rowptr), F = 602 in
+    608-float rows, columns uniform over K = 4096 rows (a 1 MB slice per XCD: every gather an
+    L2 / L1 hit). Its algorithmic rate is the ceiling of the access pattern itself — 4 rows x
+    256 B per wave instruction — on this chip, measured live (HIP events, median of reps)."""
+    import re
+
+    m = re.match(r"spmm_unit_kernel<(\d+), (\d+), (\d+)", kernel_name)
+    if m is None:
+        return None
+    g, nj = int(m.group(2)), int(m.group(3))
+    M, nnz = op.shape[0], op.nnz
+    gen = torch.Generator(device=dev).manual_seed(1)
+    rows = torch.repeat_interleave(torch.arange(M, device=dev), torch.diff(op.rowptr))
+    col = torch.randint(0, K, (nnz,), device=dev, generator=gen, dtype=torch.int64)
+    col = (torch.sort(rows * K + col).values - rows * K).to(torch.int32)  # ascending per row
+    syn = cso.CsrOperand(op.rowptr, col, torch.rand(nnz, device=dev, generator=gen), (M, K))
+    X = torch.randn(K, 608, device=dev, generator=gen)[:, :602]
+    saved = {k: os.environ.get(k) for k in ("GNN_SPMM_G", "GNN_SPMM_NJ")}
+    os.environ["GNN_SPMM_G"], os.environ["GNN_SPMM_NJ"] = str(g), str(nj)
+    try:
+        cso.spmm_csr(syn, X)
+        cso.take_timing_records()
+        cso.enable_timing(True)
+        for _ in range(reps):
+            cso.spmm_csr(syn, X)
+        recs = cso.take_timing_records()
+    finally:
+        cso.enable_timing(False)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    ms = float(np.median([r[1] for r in recs]))
+    return {"GBps": round(recs[0][2] / (ms * 1e-3) / 1e9, 1), "us": round(ms * 1e3, 1), "kernel": recs[0][3],
+            "what": f"same kernel instantiation and row lengths as the layer-0 operand, columns uniform over "
+                    f"K = {K} rows (slice {K * 256 / 1e6:.1f} MB per XCD: cache-resident), median of {reps}"}
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -578,7 +619,7 @@ def main():
     log(f"end to end: {world * args.steps / e2e_s:.1f} mini-batches/s ({time.time() - t0:.1f}s)")
 
     # ------------------------------------------------- GPU step over distinct pre-sampled batches
-    gpu_step, roof, spmm_detail, staging_info = None, None, {}, None
+    gpu_step, roof, spmm_detail, staging_info, dp_ab = None, None, {}, None, None
     step_batches = []
     if not args.no_gpu_step:
         nwarm = max(2, min(args.warmup, 10))
@@ -633,6 +674,25 @@ def main():
         stager.timing = []
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
         h_bytes, h_sec = stager.take_timing()
+        dp_ab = None
+        if world > 1 and getattr(trainer, "bucketed", None) is not None:
+            # the other gradient exchange over the same batches (gnn_amd.dp vs one flat all-reduce):
+            # neither can be measured over RCCL / xGMI on a one-GPU box, so the N > 1 runs time both
+            first = "bucketed" if trainer.exchange is not None else "flat"
+            trainer.exchange = None if first == "bucketed" else trainer.bucketed
+            k_[0] = nwarm
+            torch.cuda.synchronize()
+            for j in range(len(dbs)):
+                dbs[j] = None
+                if native:
+                    pre[j].host.drop_device()
+            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps))
+            trainer.exchange = trainer.bucketed if first == "bucketed" else None
+            dp_ab = {"default": first, first: round(world * gsteps / step_s, 3),
+                     ("flat" if first == "bucketed" else "bucketed"): round(world * gsteps / alt_s, 3),
+                     "what": "gpu_step mini-batches/s over the same pre-sampled batches with each gradient "
+                             "exchange (bucketed: all-to-all per backward stage overlapped with the backward, "
+                             "then the clip factors, shard sums and one gather; flat: clip + one all-reduce)"}
         gpu_step = {"value": round(world * gsteps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / gsteps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / gsteps, 3),
@@ -651,6 +711,14 @@ def main():
         step_batches = [(lb.host, db) for lb, db in zip(pre[nwarm:], dbs[nwarm:])]
         if recs:
             roof, spmm_detail = roofline_from(recs, step_batches, args, traffic, gsteps)
+            try:  # the measured ceiling of the dominant kernel's own access shape (cache-resident)
+                dom = roof["kernel"].split(" (")[0]
+                ceil = gather_ceiling(step_batches[0][1].adjs[0], dom, dev)
+                if ceil:
+                    ceil["frac"] = round(roof["algorithmic"]["GBps"] / ceil["GBps"], 4)
+                    roof["gather_ceiling"] = ceil
+            except Exception as e:  # a failed side measurement must not sink the benchmark
+                log(f"gather ceiling skipped: {e!r}")
         if args.cprofile and rank == 0:
             import cProfile
             import pstats
@@ -724,6 +792,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,
+            "dp_exchange_ab": dp_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "spmm_per_callsite": spmm_detail,
             "sampler": sampler_cost,

@@ -1,4 +1,5 @@
-"""In-tree builds: libgnn_spmm.so (hipcc, gfx950) and libgnn_sampler.so (g++, host only).
+"""In-tree builds: libgnn_spmm.so (hipcc, gfx950), libgnn_sampler.so (g++, host only) and the
+PyTorch-ROCm extension module `spmm` (g++ against torch + libgnn_spmm.so).
 No JIT cache: the .so files live next to the package so they travel with the repository
 snapshot to the GPU box."""
 from __future__ import annotations
@@ -71,6 +72,58 @@ def build_sampler(force: bool = False, verbose: bool = False) -> str:
     return SAMPLER_OUT
 
 
+EXT_SRC = os.path.join(HERE, "csrc", "spmm_ext.cpp")
+
+
+def ext_path() -> str:
+    """The reference's native module name `spmm`, built next to the repository root so that
+    `import spmm` (custom_sparse_ops.py:8's load(name='spmm', ...)) finds it."""
+    import sysconfig
+
+    return os.path.join(REPO, "spmm" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_torch_ext(force: bool = False, verbose: bool = False) -> str:
+    """The PyTorch-ROCm extension (gnn_amd/csrc/spmm_ext.cpp): pybind module `spmm` + the
+    torch.ops.gnn operators, host C++ linked against torch and libgnn_spmm.so (built first)."""
+    import sysconfig
+
+    import torch
+    import torch.utils.cpp_extension as ce
+
+    build_library(verbose=verbose)
+    out = ext_path()
+    h = hashlib.sha1()
+    for p in (EXT_SRC, os.path.join(REPO, "include", "gnn_spmm.h")):
+        with open(p, "rb") as f:
+            h.update(f.read())
+    h.update(torch.__version__.encode())
+    bid = h.hexdigest()[:12]
+    stamp = out + ".buildid"
+    if not force and os.path.exists(out) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == bid:
+                return out
+    incs = ce.include_paths(device_type="cuda") + [sysconfig.get_paths()["include"], os.path.join(REPO, "include")]
+    libdirs = ce.library_paths(device_type="cuda")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           "-DTORCH_EXTENSION_NAME=spmm", "-DTORCH_API_INCLUDE_EXTENSION_H"]
+    cmd += [f"-I{d}" for d in incs] + [EXT_SRC, "-o", out + ".tmp"]
+    cmd += [f"-L{d}" for d in libdirs] + [f"-L{HERE}", "-lgnn_spmm", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
+                                           "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
+    cmd += [f"-Wl,-rpath,{libdirs[0]}", "-Wl,-rpath,$ORIGIN/gnn_amd"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    with open(stamp, "w") as f:
+        f.write(bid)
+    return out
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))
     print(build_sampler(force=True, verbose=True))
+    print(build_torch_ext(force=True, verbose=True))

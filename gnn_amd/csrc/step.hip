@@ -442,6 +442,13 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
                                                             HP<float>(d, GNN_SH_HEAD_GB));
     GNN_LAUNCHED("colsum_kernel");
   }
+  // gradient-ready events (GNN_SH_GRAD_EVENTS): the caller's DP exchange of a bucket starts there
+  const int64_t* const E = HP<const int64_t>(d, GNN_SH_GRAD_EVENTS);
+  auto grads_ready = [&](int64_t slot, hipStream_t s) -> int {
+    if (E && slot < E[0] && E[slot]) GNN_HIP(hipEventRecord((hipEvent_t)E[slot], s), "hipEventRecord (grad event)");
+    return 0;
+  };
+  GNN_TRY(grads_ready(1, st));
   for (int l = pl.nl - 1; l >= 0; --l) {
     LayerBufs& b = pl.lb[l];
     const int64_t N = b.N;
@@ -487,9 +494,11 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       else
         GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
                                     b.b_gemm_dw, sw));
+      GNN_TRY(grads_ready(2 + l, sw));  // sw follows st's norm backward (fork_join)
     } else {
       if (pl.sage) GNN_TRY(mm_gtx(h, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
       GNN_TRY(mm_gtx(h, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
+      GNN_TRY(grads_ready(2 + l, st));
     }
     if (l >= 1) {  // dY_{l-1} = A_lᵀ·dfeat (+ dxs through rmap: the x[sampled] gradient)
       LayerBufs& prev = pl.lb[l - 1];

@@ -24,7 +24,7 @@ from . import custom_sparse_ops as cso
 
 VERSION, MAX_LAYERS, HEADER, LAYER_SLOTS, SAGE, GCN = 1, 4, 24, 32, 0, 1
 (H_VERSION, H_LAYERS, H_KIND, H_X0, H_LDX0, H_F0, H_HEAD_W, H_HEAD_B, H_HEAD_GW, H_HEAD_GB, H_CLASSES, H_LABELS,
- H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING) = range(19)
+ H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING, H_GRAD_EVENTS) = range(20)
 TIMING_SLOTS = 16
 (L_ROWPTR, L_COL, L_VAL, L_M, L_K, L_NNZ, L_TROWPTR, L_TCOL, L_TVAL, L_SAMPLED, L_NSAMPLED, L_RMAP, L_WW, L_BW,
  L_WB, L_BB, L_SCALE, L_OFFSET, L_GWW, L_GBW, L_GWB, L_GBB, L_GSCALE, L_GOFFSET, L_SEED) = range(25)
@@ -124,7 +124,19 @@ class NativeStep:
                     return False
         return True
 
-    def step(self, x0, adjs, sampled_nodes, labels) -> torch.Tensor:
+    def grad_stages(self):
+        """Parameter indices (into self.params / the flat gradient) per backward stage, in the
+        order the step finalises them: [head, layer L-1, ..., layer 0]."""
+        head = {id(p) for p in self.model.linear.parameters()}
+        stages = [[i for i, p in enumerate(self.params) if id(p) in head]]
+        for gc in reversed(self.enc.gcs):
+            mine = {id(p) for p in gc.parameters()}
+            stages.append([i for i, p in enumerate(self.params) if id(p) in mine])
+        return stages
+
+    def step(self, x0, adjs, sampled_nodes, labels, grad_events=None) -> torch.Tensor:
+        """grad_events: optional [head event, layer 0 event, layer 1 event, ...] (torch.cuda.Event)
+        recorded on the step's stream once those gradients are final (GNN_SH_GRAD_EVENTS)."""
         model = self.model
         training = model.training
         tr = bool(training and self.p_enc > 0)
@@ -150,6 +162,15 @@ class NativeStep:
         loss = torch.empty((), dtype=torch.float32, device=x0.device)
         d[H_LOSS] = loss.data_ptr()
         timing = self._arm_timing(d, len(adjs)) if cso.timing_enabled() else None
+        E = None
+        if grad_events is not None:
+            E = np.zeros(1 + len(grad_events), dtype=np.int64)
+            E[0] = len(E)
+            for i, ev in enumerate(grad_events):
+                if ev is not None:
+                    ev.record()  # creates the underlying hipEvent; the step re-records it
+                    E[1 + i] = ev.cuda_event
+            d[H_GRAD_EVENTS] = E.ctypes.data
         L = _lib.lib()
         dp = d.ctypes.data
         wsb = L.gnn_train_step_workspace_bytes(dp)

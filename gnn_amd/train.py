@@ -4,10 +4,13 @@ Reference: per-rank threads in one process; grads flattened with torch.cat, publ
 shared list, ``threading.Barrier``, summed with P2P ``.to(device)`` copies (main.py:149-168);
 per-rank clip_grad_norm_(5) BEFORE the sum and no averaging (main.py:146,159).
 
-Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). On the
-GPU the per-rank clip writes the clipped gradients straight into one flat fp32 buffer (one
-kernel, gnn_amd.optim), summed with ONE in-place ``all_reduce(SUM)``, and Adam reads them as
-views of that buffer; at N = 1 the clip factor is applied inside the Adam launch. (On the CPU
+Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). With the
+native step executor the exchange is bucketed per backward stage and overlapped with the
+backward (gnn_amd.dp: all-to-all of unscaled shards as each stage finishes, then this rank's
+clip factor, the weighted shard sums and an all-gather — the same per-rank-clip-then-sum).
+Otherwise the per-rank clip writes the clipped gradients straight into one flat fp32 buffer
+(one kernel, gnn_amd.optim), summed with ONE in-place ``all_reduce(SUM)``, and Adam reads them
+as views of that buffer; at N = 1 the clip factor is applied inside the Adam launch. (On the CPU
 — the gloo tests — the same semantics run through torch's clip_grad_norm_ and Adam.)
 Gradients are reset to None each step, so autograd hands its freshly computed tensors over
 instead of accumulating into old ones. Initial weights are broadcast from rank 0 (the
@@ -15,6 +18,7 @@ reference never syncs them: SURVEY.md Appendix B, F).
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -60,6 +64,19 @@ class Trainer:
             self.world = torch.distributed.get_world_size(group)
         if self.world > 1:
             self.broadcast_parameters()
+        # N > 1 with the executor: the gradient exchange bucketed per backward stage and started
+        # while the backward runs (gnn_amd.dp), built whenever possible; used when
+        # GNN_DP_BUCKETS=1 (default: one flat all-reduce after the backward — bench.py times
+        # both at N > 1, since neither is measured over RCCL / xGMI on a one-GPU box)
+        self.bucketed = None
+        if self.world > 1 and self.executor is not None:
+            from .dp import BucketedExchange
+
+            try:
+                self.bucketed = BucketedExchange(self.executor, self.optimizer, group)
+            except ValueError:
+                self.bucketed = None
+        self.exchange = self.bucketed if os.environ.get("GNN_DP_BUCKETS", "0") == "1" else None
 
     @property
     def num_params(self) -> int:
@@ -87,6 +104,12 @@ class Trainer:
         if not self.model.training:  # module.train() walks every submodule: ~50 µs of host time
             self.model.train()
         if self.executor is not None and self.executor.supports(x0, adjs, sampled_nodes, labels):
+            if self.exchange is not None:  # buckets leave while the lower layers' backward runs
+                loss = self.executor.step(x0, adjs, sampled_nodes, labels, grad_events=self.exchange.events)
+                self.exchange.issue()
+                self.exchange.finish()  # this rank's clip, Σ_r c_r g_r into the flat gradient
+                self.optimizer.step(clipped=True)
+                return loss
             loss = self.executor.step(x0, adjs, sampled_nodes, labels)  # grads into the flat buffer
             if self.world > 1:
                 flat = self.optimizer.clip_to_flat()

@@ -22,7 +22,11 @@
  *     GNN_STEP_TIMING_SLOTS slots; the caller puts a hipEvent_t pair in slots 0-1 of each, and
  *     the step arms them around its aggregation kernels in call order (forward layers bottom-up,
  *     then the backward aggregations top-down) and writes slots 2-14: kind (0 fwd, 1 bwd),
- *     layer, M, K, nnz, F, padded F, ldx, ldy, X, Y (device addresses), residual rows, 1.
+ *     layer, M, K, nnz, F, padded F, ldx, ldy, X, Y (device addresses), residual rows, 1;
+ *     and optionally gradient-ready events: a HOST int64 array E, E[0] = entries, E[1] = a
+ *     hipEvent_t recorded once the head's gradients are final, E[2 + l] = one recorded once
+ *     layer l's gradients (weights, biases, scale, offset) are final (0 = none): the caller's
+ *     data-parallel exchange starts on a bucket while the backward of the layers below runs.
  *   layer l: the operand A (rowptr / col / val, M x K, nnz) and its transpose (K x M, layers >= 1),
  *     sampled (int64 [M], SAGE) and rmap (int32 [K], rmap[sampled[i]] = i, SAGE layers >= 1),
  *     weights W_W / W_B (N x F row-major), biases, scale / offset, their gradient buffers, the
@@ -50,7 +54,7 @@ enum {
   GNN_SH_VERSION = 0, GNN_SH_LAYERS = 1, GNN_SH_KIND = 2, GNN_SH_X0 = 3, GNN_SH_LDX0 = 4, GNN_SH_F0 = 5,
   GNN_SH_HEAD_W = 6, GNN_SH_HEAD_B = 7, GNN_SH_HEAD_GW = 8, GNN_SH_HEAD_GB = 9, GNN_SH_CLASSES = 10,
   GNN_SH_LABELS = 11, GNN_SH_LDL = 12, GNN_SH_HEAD_SEED = 13, GNN_SH_PDROP_BITS = 14, GNN_SH_TRAINING = 15,
-  GNN_SH_LOSS = 16, GNN_SH_NHID = 17, GNN_SH_TIMING = 18
+  GNN_SH_LOSS = 16, GNN_SH_NHID = 17, GNN_SH_TIMING = 18, GNN_SH_GRAD_EVENTS = 19
 };
 enum {
   GNN_SL_ROWPTR = 0, GNN_SL_COL = 1, GNN_SL_VAL = 2, GNN_SL_M = 3, GNN_SL_K = 4, GNN_SL_NNZ = 5,

@@ -121,10 +121,12 @@ def _native_model(seed, F, ncls, fused):
     return build_model("graphsage", F, 32, [1, 1, 1], ncls, dropout=0.0, fused=fused)
 
 
-def _native_trainer_worker(rank, world, port, q):
-    """The benchmark's N > 1 branch: executor step -> ClipAdam.clip_to_flat -> all_reduce(SUM) ->
-    step(clipped=True) (train.py, Trainer.step with the executor)."""
+def _native_trainer_worker(rank, world, port, q, buckets=True):
+    """The benchmark's N > 1 branch: the executor step, then (buckets=True, the default) the
+    bucketed exchange overlapped with the backward (gnn_amd.dp) or (buckets=False)
+    ClipAdam.clip_to_flat -> all_reduce(SUM); then Adam (train.py, Trainer.step)."""
     _env(rank, world, port)
+    os.environ["GNN_DP_BUCKETS"] = "1" if buckets else "0"
     import torch.distributed as dist
 
     try:
@@ -143,6 +145,7 @@ def _native_trainer_worker(rank, world, port, q):
         x0 = x.to(dev)[:, :F]
         assert tr.executor is not None and tr.executor.supports(x0, db.adjs, db.sampled_nodes, db.labels), \
             "the executor branch must be the one exercised"
+        assert (tr.exchange is not None) == buckets, "the exchange variant under test must be the one in use"
         losses = [float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels)) for _ in range(2)]
         torch.cuda.synchronize()
         q.put((rank, "ok", losses, [p.detach().cpu().numpy().copy() for p in net.parameters()]))
@@ -188,12 +191,18 @@ def _native_reference_two_steps():
     return [p.detach().numpy() for p in params], sums, losses
 
 
-def test_trainer_executor_dp_step_matches_reference():
-    """The branch bench.py runs at N > 1 (executor + flat clip + all_reduce + Adam on views),
-    with GPU-extracted CsrOperands as the bench feeds them, against main.py:146-170 semantics."""
-    out = _spawn(_native_trainer_worker)
+_native_out = {}
+
+
+@pytest.mark.parametrize("buckets", [True, False], ids=["bucketed", "flat"])
+def test_trainer_executor_dp_step_matches_reference(buckets):
+    """The branch bench.py runs at N > 1 (executor + the gradient exchange + Adam on views), with
+    GPU-extracted CsrOperands as the bench feeds them, against main.py:146-170 semantics — for the
+    bucketed exchange overlapped with the backward (the default) and the flat all-reduce."""
+    out = _spawn(_native_trainer_worker, extra=(buckets,))
     for rank, status, _, _ in out:
         assert status == "ok", f"rank {rank}: {status}"
+    _native_out[buckets] = out
     ref, sums, ref_losses = _native_reference_two_steps()
     for rank in range(2):
         for s in range(2):
@@ -251,13 +260,13 @@ def _exchange_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def _spawn(fn, world=2):
+def _spawn(fn, world=2, extra=()):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=fn, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -321,3 +330,16 @@ def test_peer_exchange_hip_gathers_bit_exact():
     out = _spawn(_exchange_worker)
     for rank, status, _, _ in out:
         assert status == "ok", f"rank {rank}: {status}"
+
+
+def test_bucketed_exchange_equals_flat():
+    """At world size 2 the bucketed exchange's sum (c_0 g_0 + c_1 g_1 per element, each product
+    rounded once) is the flat all-reduce's, bit for bit."""
+    for b in (True, False):
+        if b not in _native_out:
+            out = _spawn(_native_trainer_worker, extra=(b,))
+            assert all(st == "ok" for _, st, _, _ in out), out
+            _native_out[b] = out
+    for rank in range(2):
+        for a, c in zip(_native_out[True][rank][3], _native_out[False][rank][3]):
+            assert np.array_equal(a, c), "bucketed and flat exchanges disagree"

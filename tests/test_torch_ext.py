@@ -1,0 +1,146 @@
+"""The PyTorch-ROCm extension (gnn_amd/csrc/spmm_ext.cpp): the reference's native module `spmm`
+(spmm_cpp/spmm.cpp:52-56, loaded by custom_sparse_ops.py:8) and the registered operators
+torch.ops.gnn.* (fake kernels + autograd from gnn_amd/torch_ops.py).
+
+CPU: the module imports as `spmm` with the reference's three functions; the operators' schemas
+and fake (shape) kernels; the reference's TORCH_CHECK messages (spmm.cpp:10-21).
+GPU: `spmm.spmm_load_balance` / `spmm_naive` / `create_coo_tensor` against the C oracle (operand
+values bit-exact; aggregation within the module tolerance), torch.ops.gnn.spmm forward + backward
+against the oracle (backward = Aᵀ·G, custom_sparse_ops.py:33-37), and a function using the op
+compiled with torch.compile(fullgraph=True) (dynamo + AOTAutograd trace the op through its fake
+kernel and autograd formula) equal to eager, outputs and gradients.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gnn_amd import torch_ops
+from oracle.fixtures import random_csr
+
+RTOL = ATOL = 1e-5  # the aggregation tolerance of every parity test
+
+
+def test_module_and_ops_registered():
+    mod = torch_ops.load()
+    assert mod.__name__ == "spmm"
+    for name in ("spmm_load_balance", "spmm_naive", "create_coo_tensor"):
+        assert callable(getattr(mod, name))
+    for op in ("spmm", "spmm_csr", "csr_transpose"):
+        assert hasattr(torch.ops.gnn, op)
+    s = str(torch.ops.gnn.spmm.default._schema)
+    assert s.startswith("gnn::spmm(Tensor rowptr, Tensor col, Tensor val, Tensor t_rowptr")
+
+
+def test_fake_kernels_shapes():
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    torch_ops.load()
+    with FakeTensorMode():
+        rp = torch.empty(11, dtype=torch.int32, device="cuda")
+        c = torch.empty(30, dtype=torch.int32, device="cuda")
+        v = torch.empty(30, device="cuda")
+        x = torch.empty(7, 5, device="cuda")
+        y = torch.ops.gnn.spmm(rp, c, v, rp, c, v, 10, 7, x)
+        assert tuple(y.shape) == (10, 5) and y.dtype == torch.float32
+        t = torch.ops.gnn.csr_transpose(rp, c, v, 10, 7)
+        assert [tuple(a.shape) for a in t] == [(8,), (30,), (30,)]
+
+
+def test_reference_error_messages():
+    mod = torch_ops.load()
+    A = torch.eye(3).to_sparse()
+    with pytest.raises(RuntimeError, match="sparseMat must be a CUDA tensor"):
+        mod.spmm_load_balance(A, torch.zeros(3, 2))
+    with pytest.raises(RuntimeError, match="must be CUDA tensors"):
+        mod.create_coo_tensor(torch.zeros(4, dtype=torch.int32), torch.zeros(4, dtype=torch.int32),
+                              torch.zeros(0, dtype=torch.int16), torch.zeros(3), 3, 3)
+
+
+def _case(seed, M=300, K=500, F=602):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 120, M)
+    lens[5] = 0
+    lens[9] = K  # a dense row: cut across work units
+    full, rowptr, col, normfact = random_csr(M, K, lens, rng)
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    G = rng.standard_normal((M, F)).astype(np.float32)
+    return full, rowptr, col, normfact, X, G
+
+
+@pytest.mark.gpu
+def test_module_functions_vs_oracle(dev):
+    mod = torch_ops.load()
+    full, rowptr, col, normfact, X, _ = _case(1)
+    M, K = len(rowptr) - 1, X.shape[0]
+    t = lambda a: torch.from_numpy(a).to(dev)
+    A = mod.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int16)), t(normfact), M, K)
+    assert A.is_sparse and A.is_coalesced() and tuple(A.shape) == (M, K)
+    ocol, oval = O.build_operand(full, rowptr, col, normfact)
+    idx = A._indices().cpu().numpy()
+    assert np.array_equal(idx[1], ocol) and np.array_equal(np.diff(np.searchsorted(idx[0], np.arange(M + 1))),
+                                                           np.diff(rowptr))
+    assert np.array_equal(A._values().cpu().numpy().view(np.uint32), oval.view(np.uint32)), "values bit-exact"
+    want = O.spmm_f32(rowptr, ocol, oval, X)
+    for fn in (mod.spmm_load_balance, mod.spmm_naive):
+        Y = fn(A, t(X))
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(Y.cpu().numpy(), want, rtol=RTOL, atol=ATOL)
+    with pytest.raises(RuntimeError, match="denseMat must be contiguous"):
+        mod.spmm_load_balance(A, t(np.ascontiguousarray(X.T)).T)
+    with pytest.raises(RuntimeError, match="sparseMat must be coalesced"):
+        B = torch.sparse_coo_tensor(A._indices().flip(1), A._values().flip(0), A.shape)
+        mod.spmm_load_balance(B, t(X))
+
+
+def _csr_pieces(dev, seed):
+    from gnn_amd import custom_sparse_ops as cso
+
+    full, rowptr, col, normfact, X, G = _case(seed)
+    M, K = len(rowptr) - 1, X.shape[0]
+    t = lambda a: torch.from_numpy(a).to(dev)
+    op, _ = cso.build_operand(t(full), t(rowptr), t(col), t(normfact), M, K, with_coo=False)
+    return op, X, G, (rowptr, *O.build_operand(full, rowptr, col, normfact))
+
+
+@pytest.mark.gpu
+def test_registered_op_forward_backward_vs_oracle(dev):
+    torch_ops.load()
+    op, X, G, (rowptr, ocol, oval) = _csr_pieces(dev, 2)
+    M, K = op.shape
+    Xd = torch.from_numpy(X).to(dev).requires_grad_(True)
+    Y = torch_ops.spmm(op, Xd)
+    Y.backward(torch.from_numpy(G).to(dev))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Y.detach().cpu().numpy(), O.spmm_f32(rowptr, ocol, oval, X), rtol=RTOL, atol=ATOL)
+    trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K)
+    np.testing.assert_allclose(Xd.grad.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
+    # the operator's own transpose is the canonical one, bit for bit
+    r, c, v = torch.ops.gnn.csr_transpose(op.rowptr, op.col, op.val, M, K)
+    assert np.array_equal(r.cpu().numpy(), trp) and np.array_equal(c.cpu().numpy(), trc)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), trv.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_torch_compile_traces_the_op(dev):
+    torch_ops.load()
+    op, X, G, _ = _csr_pieces(dev, 3)
+    t = op.transpose()
+    M, K = op.shape
+    W = torch.randn(X.shape[1], 64, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
+
+    def layer(x, w):  # GraphSAGE-like: aggregate, project, activate
+        h = torch.ops.gnn.spmm(op.rowptr, op.col, op.val, t.rowptr, t.col, t.val, M, K, x)
+        return torch.nn.functional.elu(h @ w)
+
+    compiled = torch.compile(layer, backend="aot_eager", fullgraph=True)
+    outs = []
+    for fn in (layer, compiled):
+        x = torch.from_numpy(X).to(dev).requires_grad_(True)
+        w = W.clone().requires_grad_(True)
+        y = fn(x, w)
+        y.sum().backward()
+        torch.cuda.synchronize()
+        outs.append((y.detach(), x.grad, w.grad))
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
