@@ -35,6 +35,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <string>
 
 #include "common.h"
 #include "gnn_layers.h"
@@ -152,9 +153,31 @@ int fork_join(Aux* a, hipStream_t from, hipStream_t to) {
 bool no_index() {
   static const bool on = [] {
     const char* e = getenv("GNN_STEP_GATHER");
-    return e && atoi(e) != 0;
+    const char* a = getenv("GNN_GEMM_ALGO");
+    return (e && atoi(e) != 0) || (a && std::string(a) == "f32");  // the f32 kernel has no indexed form
   }();
   return on;
+}
+
+// GNN_GEMM_ALGO=f32: the layer GEMMs on the f32-input MFMA kernel (gnn_gemm_f32, exact fp32)
+// instead of split3 — the same routing, x[sampled] gathered (no row-indexed operands), no aux
+// stream. For the end-to-end A/B of the two kernels (gnn_amd.fused reads the same variable).
+bool f32_gemm() {
+  static const bool on = [] {
+    const char* e = getenv("GNN_GEMM_ALGO");
+    return e && std::string(e) == "f32";
+  }();
+  return on;
+}
+
+int gemm(int ak, int bk, int64_t M, int64_t N, int64_t K, int nb, const float* const* A, int64_t lda,
+         const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* ws, size_t wsb, hipStream_t st) {
+  if (f32_gemm()) return gnn_gemm_f32(ak, bk, M, N, K, nb, A, lda, B, ldb, C, ldc, ws, wsb, st);
+  return gnn_gemm_f32_split3(ak, bk, M, N, K, nb, A, lda, B, ldb, C, ldc, ws, wsb, st);
+}
+
+size_t gemm_ws(int64_t M, int64_t N, int64_t K, int nb) {
+  return std::max(gnn_gemm_f32_split3_workspace_bytes(M, N, K, nb), gnn_gemm_f32_workspace_bytes(M, N, K, nb));
 }
 
 // GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
@@ -254,7 +277,7 @@ int plan(const int64_t* d, Arena& ar, Plan& pl) {
     b.rstd = ar.take<float>(b.M);
     b.b_fwd = gnn_spmm_workspace_bytes(b.M, b.nnz, b.Fk, 0);
     b.ws_fwd = ar.take<char>((int64_t)b.b_fwd);
-    b.b_gemm_f = gnn_gemm_f32_split3_workspace_bytes(b.M, N, b.F, n);
+    b.b_gemm_f = gemm_ws(b.M, N, b.F, n);
     b.ws_gemm_f = ar.take<char>((int64_t)b.b_gemm_f);
     b.ws_gemm_f2 = pl.sage ? ar.take<char>((int64_t)b.b_gemm_f) : nullptr;  // the aux stream's product
   }
@@ -277,12 +300,12 @@ int plan(const int64_t* d, Arena& ar, Plan& pl) {
     b.dhW = ar.take<float>(b.M * N);
     b.b_norm = gnn_sage_norm_bwd_workspace_bytes(b.M, b.D);
     b.ws_norm = ar.take<char>((int64_t)b.b_norm);
-    b.b_gemm_dw = gnn_gemm_f32_split3_workspace_bytes(N, b.F, b.M, n);
+    b.b_gemm_dw = gemm_ws(N, b.F, b.M, n);
     b.ws_gemm_dw = ar.take<char>((int64_t)b.b_gemm_dw);
     if (l >= 1) {
       b.dxs = pl.sage ? ar.take<float>(b.M * b.F) : nullptr;
       b.dfeat = ar.take<float>(b.M * b.F);
-      b.b_gemm_dx = gnn_gemm_f32_split3_workspace_bytes(b.M, b.F, N, n);
+      b.b_gemm_dx = gemm_ws(b.M, b.F, N, n);
       b.ws_gemm_dx = ar.take<char>((int64_t)b.b_gemm_dx);
       b.b_bwd = gnn_spmm_workspace_bytes(b.K, b.nnz, b.F, 0);
       b.ws_bwd = ar.take<char>((int64_t)b.b_bwd);
@@ -341,7 +364,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
   }();
   const int training = (int)d[GNN_SH_TRAINING];
   Aux* aux = nullptr;
-  if (overlap_enabled()) GNN_TRY(aux_of(st, &aux));
+  if (overlap_enabled() && !f32_gemm()) GNN_TRY(aux_of(st, &aux));
   std::unique_lock<std::mutex> aux_lock;
   if (aux) aux_lock = std::unique_lock<std::mutex>(aux->mu);
   bool aux_used = false;
@@ -414,7 +437,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       const float* A[2] = {pl.sage ? b.xs : b.feat, b.feat};
       const float* B[2] = {pl.sage ? WB : WW, WW};
       float* Cc[2] = {pl.sage ? b.hB : b.hW, b.hW};
-      GNN_TRY(gnn_gemm_f32_split3(0, 0, b.M, N, b.F, n, A + (pl.sage ? 0 : 1), b.ldo, B + (pl.sage ? 0 : 1), b.F,
+      GNN_TRY(gemm(0, 0, b.M, N, b.F, n, A + (pl.sage ? 0 : 1), b.ldo, B + (pl.sage ? 0 : 1), b.F,
                                   Cc + (pl.sage ? 0 : 1), N, b.ws_gemm_f, b.b_gemm_f, st));
     } else {
       if (pl.sage) GNN_TRY(mm_xwt(h, b.xs, b.ldo, WB, b.F, b.hB, N, b.M, N, b.F));
@@ -467,7 +490,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       if (ok && fills(b.M, b.F, n)) {
         const float* B[2] = {pl.sage ? WB : WW, WW};
         float* Cc[2] = {pl.sage ? b.dxs : b.dfeat, b.dfeat};
-        GNN_TRY(gnn_gemm_f32_split3(0, 1, b.M, b.F, N, n, G + o, N, B + o, b.F, Cc + o, b.F, b.ws_gemm_dx,
+        GNN_TRY(gemm(0, 1, b.M, b.F, N, n, G + o, N, B + o, b.F, Cc + o, b.F, b.ws_gemm_dx,
                                     b.b_gemm_dx, st));
       } else {
         if (pl.sage) GNN_TRY(mm_gw(h, b.dhB, N, WB, b.F, b.dxs, b.F, b.M, b.F, N));
@@ -492,7 +515,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
         GNN_TRY(gnn::gemm_split3_indexed(1, 1, N, b.F, b.M, n, G + o, N, nullptr, 0, X + o, b.ldo, IB + o, b.K,
                                          Cc + o, b.F, b.ws_gemm_dw, b.b_gemm_dw, sw));
       else
-        GNN_TRY(gnn_gemm_f32_split3(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
+        GNN_TRY(gemm(1, 1, N, b.F, b.M, n, G + o, N, X + o, b.ldo, Cc + o, b.F, b.ws_gemm_dw,
                                     b.b_gemm_dw, sw));
       GNN_TRY(grads_ready(2 + l, sw));  // sw follows st's norm backward (fork_join)
     } else {
