@@ -685,10 +685,11 @@ def main():
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
         h_bytes, h_sec = stager.take_timing()
         dp_ab = None
-        if world > 1 and getattr(trainer, "bucketed", None) is not None and os.environ.get("GNN_BENCH_DP_AB") == "1":
-            # the other gradient exchange over the same batches (gnn_amd.dp vs one flat all-reduce):
-            # neither can be measured over RCCL / xGMI on a one-GPU box (opt-in: the default N > 1
-            # run keeps to the exchange it reports)
+        if world > 1 and getattr(trainer, "bucketed", None) is not None and os.environ.get("GNN_BENCH_DP_AB", "1") == "1":
+            # the other gradient exchange over the same batches (gnn_amd.dp vs one flat all-reduce),
+            # after the reported passes (`value` and `gpu_step` keep the default exchange): RCCL over
+            # xGMI cannot be measured on a one-GPU box, so every N > 1 run records both
+            # (GNN_BENCH_DP_AB=0 skips it). Both exchanges are tested equal (tests/test_dist_gpu.py).
             first = "bucketed" if trainer.exchange is not None else "flat"
             trainer.exchange = None if first == "bucketed" else trainer.bucketed
             k_[0] = nwarm

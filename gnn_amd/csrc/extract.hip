@@ -27,19 +27,21 @@
 //  * The kept entries leave compacted (ballot + mbcnt) into a GAPPED buffer at the chunk's own
 //    entry position (a chunk keeps at most its range), with the chunk's count; A's row pointer
 //    gets, for each segment starting in the chunk, the kept entries of the chunk before it.
-//  * A scan of the chunk counts (one workgroup per side) and a compaction pass (a wave per chunk:
-//    coalesced copies of a few hundred entries to the chunk's prefix, rowptr += prefix) finish.
+//  * The last chunk to finish in each group of 64 publishes the group's total (an agent-scope
+//    counter, write-through count words); a compaction pass (a wave per chunk: its prefix from
+//    the lower chunks of its group + the lower groups' totals, coalesced copies of its entries to
+//    that prefix, rowptr += prefix) finishes.
 //    Measured on the Reddit layer 0 (13 M graph entries with the transpose): a single walk that
 //    waited for the lower chunks' counts (chained or two-level prefix) spent ~45 % of its time
 //    waiting — every wave of a launch ends its walk at about the same time — while the gapped
 //    buffer costs one extra coalesced read and write of the kept entries (~29 MB).
 //  * Membership: a bitmap of the sorted id set with a rank per 32-bit word, one 8-byte load per
 //    lookup (built from the sorted list without atomics: rank[w] = lower_bound(ids, 32 w)). When
-//    the table fits 64 KB (N <= 262 k: Reddit) every workgroup of 12 waves copies it into LDS
+//    the table fits 64 KB (N <= 262 k: Reddit) every workgroup of 16 waves copies it into LDS
 //    first: the lookups are random 8-byte reads, one cache line each from global memory (the
 //    walk's main cost), a few LDS cycles each from the copy (layer 0: 148 -> 128 us).
-// Launches: 1. prep (tables, segment positions, chunk -> first segment) 2. walk 3. scan
-// 4. compact. Every size the host needs (grid, workspace) follows from the host-known nnz and
+// Launches: 1. prep (tables, segment positions, chunk -> first segment) 2. walk 3. compact.
+// Every size the host needs (grid, workspace) follows from the host-known nnz and
 // segment totals; no state survives a call. If the device's kept count differs from the host's
 // nnz the error flag is raised, writes stay below nnz, the tail of the outputs is zero-filled and
 // rowptr is clamped to nnz, so a consumer never reads outside the operand.

@@ -1,6 +1,6 @@
-"""GPU, world_size 2: the data-parallel step the benchmark runs at N > 1, on the one GPU.
+"""GPU, world_size 2 (and 4): the data-parallel step the benchmark runs at N > 1, on the one GPU.
 
-Both ranks run on cuda:0 with GNN_DIST_BACKEND=gloo (RCCL refuses two ranks on one GPU;
+All ranks run on cuda:0 with GNN_DIST_BACKEND=gloo (RCCL refuses two ranks on one GPU;
 gloo moves the same CUDA tensors through the host), spawned as fresh processes.
 
 * Trainer on CUDA: the native branch — ClipAdam.clip_to_flat (this rank's clip_grad_norm_(5)
@@ -14,6 +14,9 @@ gloo moves the same CUDA tensors through the host), spawned as fresh processes.
   the fp32 noise level are excluded, as in tests/test_fused_gpu.py).
 * PeerExchange with the HIP gathers: every rank receives exactly the rows it requested from
   the peer's GPU buffer (bit-exact), through the per-step host negotiation + all_to_all.
+* The benchmark's own N > 1 branch (native step executor on GPU-extracted CsrOperands) with the
+  flat all-reduce and with the bucketed exchange (gnn_amd/dp.py) against the same semantics;
+  bucketed ≡ flat bit for bit at world 2; the bucketed exchange at world 4 (uneven shards).
 """
 import os
 import socket
@@ -97,7 +100,7 @@ NSPEC = dict(name="dist-native", num_nodes=6000, num_edge_samples=40_000, num_fe
 NSAMP, NBS = 700, 64
 
 
-def _native_batch(rank, device_extract):
+def _native_batch(rank, device_extract, world=2):
     """Rank `rank`'s batch of the native-executor case: LADIES with the lower layers extracted on
     the GPU (device_extract=True: CsrOperands + transposes + row maps, what the bench feeds the
     executor) or on the host (the CPU reference's operands; the draw is identical)."""
@@ -107,7 +110,7 @@ def _native_batch(rank, device_extract):
     A, labels, feats, ncls, train, *_ = graphs.make_dataset(spec, seed=3)
     lap = graphs.lap_matrix(A, "graphsage")
     N = A.shape[0]
-    chunk = sampler.rank_batches(train, NBS, rank, 2, 1)[0]
+    chunk = sampler.rank_batches(train, NBS, rank, world, 1)[0]
     hb = sampler.ladies_sample_host(50 + rank, chunk, np.array([NSAMP] * 5), N, lap, labels, [1, 1, 1],
                                     np.full(N, -1, np.int64), np.zeros(N, np.int64), None, 1.0, [0],
                                     device_extract=device_extract)
@@ -122,8 +125,8 @@ def _native_model(seed, F, ncls, fused):
 
 
 def _native_trainer_worker(rank, world, port, q, buckets=True):
-    """The benchmark's N > 1 branch: the executor step, then (buckets=True, the default) the
-    bucketed exchange overlapped with the backward (gnn_amd.dp) or (buckets=False)
+    """The benchmark's N > 1 branch: the executor step, then (buckets=True, GNN_DP_BUCKETS=1) the
+    bucketed exchange overlapped with the backward (gnn_amd.dp) or (buckets=False, the default)
     ClipAdam.clip_to_flat -> all_reduce(SUM); then Adam (train.py, Trainer.step)."""
     _env(rank, world, port)
     os.environ["GNN_DP_BUCKETS"] = "1" if buckets else "0"
@@ -135,7 +138,7 @@ def _native_trainer_worker(rank, world, port, q, buckets=True):
 
         init_distributed()
         dev = torch.device("cuda", 0)
-        hb, feats, ncls = _native_batch(rank, True)
+        hb, feats, ncls = _native_batch(rank, True, world)
         F = feats.shape[1]
         net = _native_model(200 + rank, F, ncls, True).to(dev)  # rank-specific init: the broadcast fixes it
         tr = Trainer(net, LR, dev)
@@ -157,24 +160,25 @@ def _native_trainer_worker(rank, world, port, q, buckets=True):
             dist.destroy_process_group()
 
 
-def _native_reference_two_steps():
+def _native_reference_two_steps(world=2):
     """main.py:146-170 on the CPU for the native case: per-rank grads of the host-extracted
     batches through the CPU branch (torch.sparse.mm), per-rank clip_grad_norm_(5), SUM, Adam."""
     from gnn_amd.models import loss as loss_fn
 
-    batches = [_native_batch(r, False) for r in range(2)]
+    batches = [_native_batch(r, False, world) for r in range(world)]
     F, ncls = batches[0][1].shape[1], batches[0][2]
-    nets = [_native_model(200, F, ncls, False) for _ in range(2)]  # rank 0's init on both
+    nets = [_native_model(200, F, ncls, False) for _ in range(world)]  # rank 0's init on all
     params = list(nets[0].parameters())
     opt = torch.optim.Adam(params, lr=LR)
     inputs = [hb.cpu_inputs(feats) for hb, feats, _ in batches]
     sums, losses = [], []
     for _ in range(2):
         with torch.no_grad():
-            for p0, p1 in zip(nets[0].parameters(), nets[1].parameters()):
-                p1.copy_(p0)
+            for net in nets[1:]:
+                for p0, p1 in zip(nets[0].parameters(), net.parameters()):
+                    p1.copy_(p0)
         grads = []
-        for r in range(2):
+        for r in range(world):
             net = nets[r]
             net.zero_grad()
             adjs, x0, sampled, y = inputs[r]
@@ -183,7 +187,7 @@ def _native_reference_two_steps():
             losses.append(float(lo.detach()))
             torch.nn.utils.clip_grad_norm_(net.parameters(), 5)
             grads.append([p.grad.detach().clone() for p in net.parameters()])
-        total = [a + b for a, b in zip(*grads)]
+        total = [sum(gs[1:], gs[0]) for gs in zip(*grads)]
         for p, g in zip(params, total):
             p.grad = g
         sums.append(total)
@@ -198,7 +202,7 @@ _native_out = {}
 def test_trainer_executor_dp_step_matches_reference(buckets):
     """The branch bench.py runs at N > 1 (executor + the gradient exchange + Adam on views), with
     GPU-extracted CsrOperands as the bench feeds them, against main.py:146-170 semantics — for the
-    bucketed exchange overlapped with the backward (the default) and the flat all-reduce."""
+    bucketed exchange overlapped with the backward and the flat all-reduce (the default)."""
     out = _spawn(_native_trainer_worker, extra=(buckets,))
     for rank, status, _, _ in out:
         assert status == "ok", f"rank {rank}: {status}"
@@ -343,3 +347,31 @@ def test_bucketed_exchange_equals_flat():
     for rank in range(2):
         for a, c in zip(_native_out[True][rank][3], _native_out[False][rank][3]):
             assert np.array_equal(a, c), "bucketed and flat exchanges disagree"
+
+
+def _check_against_reference(out, world):
+    ref, sums, ref_losses = _native_reference_two_steps(world)
+    for rank in range(world):
+        for s in range(2):
+            got, want = out[rank][2][s], ref_losses[world * s + rank]
+            assert abs(got - want) <= 1e-4 * abs(want) + 1e-6, (rank, s, got, want)
+    for r in range(1, world):
+        for a, b in zip(out[0][3], out[r][3]):
+            assert np.array_equal(a, b), f"rank {r} disagrees with rank 0 after the summed update"
+    for i, (got, want) in enumerate(zip(out[0][3], ref)):
+        sure = np.ones(got.shape, bool)
+        for s in sums:
+            gg = s[i].numpy()
+            sure &= np.abs(gg) > 1e-4 * max(np.abs(gg).max(), 1e-12)
+        assert sure.mean() > 0.5
+        np.testing.assert_allclose(got[sure], want[sure], rtol=1e-4, atol=1e-6, err_msg=f"param {i}")
+
+
+def test_bucketed_exchange_world4():
+    """Four ranks on the one GPU (gloo): uneven shards of every bucket (the bucket sizes are not
+    multiples of 4), four clip factors riding with the last bucket, the gather of four ranks'
+    shards — every rank ends with the same parameters, main.py:146-170 semantics."""
+    out = _spawn(_native_trainer_worker, world=4, extra=(True,))
+    for rank, status, _, _ in out:
+        assert status == "ok", f"rank {rank}: {status}"
+    _check_against_reference(out, 4)
