@@ -99,6 +99,9 @@ def parse():
                          "(gnn_colcount_*, the graph resident in HBM); the draw itself stays on the host. auto: "
                          "gpu from 1 M nodes (A/B on one box: ogbn-products-shaped 363 -> 720 mini-batches/s end "
                          "to end; Reddit-shaped 558 host vs 516 gpu, where the host draw is not the bound)")
+    ap.add_argument("--peer-rows", default=os.environ.get("GNN_PEER_ROWS", "alltoall"), choices=["alltoall", "direct"],
+                    help="N > 1: peer feature rows by an RCCL all-to-all per batch (default) or read directly "
+                         "from the peers' buffers over xGMI (IPC-mapped once)")
     ap.add_argument("--numa", default="off", choices=["gpu", "off"],
                     help="confine the process (training + producer threads) to the CPUs of the GPU's NUMA node "
                          "(A/B on one box, 3 runs each: 572 vs 584 mini-batches/s unpinned, so off by default)")
@@ -535,7 +538,17 @@ def main():
     torch.cuda.set_device(dev)
 
     store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank, zero_copy=args.staging == "zerocopy")
-    exchange = staging.PeerExchange() if world > 1 else None
+    exchange = direct = alltoall = None
+    if world > 1:
+        alltoall = staging.PeerExchange()
+        if args.peer_rows == "direct" or os.environ.get("GNN_BENCH_PEER_AB", "1") == "1":
+            try:  # collective; every rank gets the same outcome
+                direct = staging.PeerDirect(store, feats=feats, buffer_nodes=pl.gpu_buffer_group)
+            except RuntimeError as e:
+                log(f"{e} -> peer rows by all-to-all")
+        if args.peer_rows == "direct" and direct is None:
+            args.peer_rows = "alltoall"
+        exchange = direct if args.peer_rows == "direct" else alltoall
     stager = staging.Stager(store, exchange)
     torch.manual_seed(0)
     model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
@@ -614,7 +627,8 @@ def main():
         sampler.device_graph(loader.graph, dev)
         torch.cuda.synchronize()
     it = loader.forever()
-    if exchange is not None:  # each batch's peer negotiation off the training thread, 4 batches ahead
+    if exchange is not None and exchange.needs_negotiation:
+        # each batch's peer negotiation off the training thread, 4 batches ahead
         it = staging.NegotiatedStream(it, exchange, depth=4)
 
     def nxt_live():
@@ -629,14 +643,14 @@ def main():
     log(f"end to end: {world * args.steps / e2e_s:.1f} mini-batches/s ({time.time() - t0:.1f}s)")
 
     # ------------------------------------------------- GPU step over distinct pre-sampled batches
-    gpu_step, roof, spmm_detail, staging_info, dp_ab = None, None, {}, None, None
+    gpu_step, roof, spmm_detail, staging_info, dp_ab, peer_ab = None, None, {}, None, None, None
     step_batches = []
     if not args.no_gpu_step:
         nwarm = max(2, min(args.warmup, 10))
         gsteps = max(1, min(args.steps, args.gpu_step_batches))
         pre = [next(it) for _ in range(nwarm + gsteps)]
         loader.close()
-        if exchange is not None:
+        if isinstance(it, staging.NegotiatedStream):
             # the look-ahead negotiations finish before the passes below re-negotiate these plans on
             # this thread (Stager.issue): never two threads' collectives on the metadata group
             it.close()
@@ -705,6 +719,25 @@ def main():
                      "what": "gpu_step mini-batches/s over the same pre-sampled batches with each gradient "
                              "exchange (bucketed: all-to-all per backward stage overlapped with the backward, "
                              "then the clip factors, shard sums and one gather; flat: clip + one all-reduce)"}
+        peer_ab = None
+        if world > 1 and direct is not None and os.environ.get("GNN_BENCH_PEER_AB", "1") == "1":
+            # the other peer-row form over the same batches (direct reads of the IPC-mapped peer
+            # buffers vs the negotiated RCCL all-to-all), after the reported passes
+            other = alltoall if exchange is direct else direct
+            stager.exchange = other
+            k_[0] = nwarm
+            torch.cuda.synchronize()
+            for j in range(len(dbs)):
+                dbs[j] = None
+                if native:
+                    pre[j].host.drop_device()
+            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps))
+            stager.exchange = exchange
+            peer_ab = {"default": args.peer_rows, args.peer_rows: round(world * gsteps / step_s, 3),
+                       ("alltoall" if exchange is direct else "direct"): round(world * gsteps / alt_s, 3),
+                       "what": "gpu_step mini-batches/s over the same pre-sampled batches with each peer-row form "
+                               "(direct: gather kernels reading the peers' IPC-mapped buffers over xGMI; alltoall: "
+                               "host negotiation + gather + RCCL all_to_all_single + scatter)"}
         gpu_step = {"value": round(world * gsteps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / gsteps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / gsteps, 3),
@@ -747,9 +780,11 @@ def main():
                 st.sort_stats("cumulative").print_stats(45)
     else:
         loader.close()
-        if exchange is not None:
+        if isinstance(it, staging.NegotiatedStream):
             it.close()
     final_loss = float(loss.item()) if loss is not None else float("nan")
+    if direct is not None:
+        direct.close()  # every rank's staging is done before any buffer is unmapped / freed
     if dx:  # every GPU extraction of the run agreed with the host's counts (syncs; outside the timings)
         sampler.device_graph(loader.graph, dev).check()
 
@@ -796,6 +831,7 @@ def main():
                        "global_batch": args.batch_size * world, "samp_num": args.samp_num, "nhid": args.nhid,
                        "feat_dim": int(store.F), "num_nodes": int(N), "graph_nnz": int(A.nnz),
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
+                       "peer_rows": (args.peer_rows if world > 1 else None),
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
@@ -805,6 +841,7 @@ def main():
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,
             "dp_exchange_ab": dp_ab,
+            "peer_rows_ab": peer_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "spmm_per_callsite": spmm_detail,
             "sampler": sampler_cost,

@@ -49,6 +49,9 @@ _SIGNATURES = {
     "gnn_host_register": (_INT, [_VP, _SZ]),
     "gnn_host_unregister": (_INT, [_VP]),
     "gnn_memcpy_h2d_async": (_INT, [_VP, _VP, _SZ, _VP]),
+    "gnn_ipc_export": (_INT, [_VP, _VP, ctypes.POINTER(_I64)]),
+    "gnn_ipc_open": (_INT, [_VP, _I64, _INT, ctypes.POINTER(_VP)]),
+    "gnn_ipc_close": (_INT, [_VP, _I64]),
     # include/gnn_layers.h
     "gnn_sage_norm_fwd_f32": (_INT, [_VP, _I64, _I64, _VP, _I64, _I64, _VP, _VP, _VP, _VP, _I64, ctypes.c_float,
                                      ctypes.c_uint64, _INT, _VP, _I64, _VP, _VP, _VP]),

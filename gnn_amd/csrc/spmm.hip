@@ -26,6 +26,7 @@
 #include <climits>
 #include <cstdarg>
 #include <cstdint>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -1620,6 +1621,45 @@ int gnn_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream)
   if (bytes == 0) return 0;
   GNN_REQUIRE(dst && src, "gnn_memcpy_h2d_async: NULL pointer");
   GNN_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream), "hipMemcpyAsync");
+  return 0;
+}
+
+int gnn_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out) {
+  GNN_REQUIRE(ptr && handle_out && offset_out, "gnn_ipc_export: NULL argument");
+  static_assert(sizeof(hipIpcMemHandle_t) == GNN_IPC_HANDLE_BYTES, "IPC handle size");
+  void* base = nullptr;
+  size_t size = 0;
+  GNN_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(ptr)), "hipMemGetAddressRange");
+  hipIpcMemHandle_t h;
+  GNN_HIP(hipIpcGetMemHandle(&h, base), "hipIpcGetMemHandle");
+  std::memcpy(handle_out, &h, sizeof(h));
+  *offset_out = (int64_t)((const char*)ptr - (const char*)base);
+  return 0;
+}
+
+int gnn_ipc_open(const void* handle, int64_t offset, int peer_device, void** ptr_out) {
+  GNN_REQUIRE(handle && ptr_out && offset >= 0, "gnn_ipc_open: bad argument");
+  int cur = 0;
+  GNN_HIP(hipGetDevice(&cur), "hipGetDevice");
+  if (peer_device >= 0 && peer_device != cur) {
+    int can = 0;
+    GNN_HIP(hipDeviceCanAccessPeer(&can, cur, peer_device), "hipDeviceCanAccessPeer");
+    GNN_REQUIRE(can, "gnn_ipc_open: this GPU cannot access the peer GPU's memory");
+    const hipError_t e = hipDeviceEnablePeerAccess(peer_device, 0);
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    else GNN_HIP(e, "hipDeviceEnablePeerAccess");
+  }
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  void* base = nullptr;
+  GNN_HIP(hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  *ptr_out = (char*)base + offset;
+  return 0;
+}
+
+int gnn_ipc_close(void* ptr, int64_t offset) {
+  GNN_REQUIRE(ptr && offset >= 0, "gnn_ipc_close: bad argument");
+  GNN_HIP(hipIpcCloseMemHandle((char*)ptr - offset), "hipIpcCloseMemHandle");
   return 0;
 }
 

@@ -302,6 +302,13 @@ class NativeBatch:
         host = rows.view(-1, ld) if self._count(bb + B_HOST_ROWS) else self._d(bb + B_HOST_SRC, _I64)
         return (self._d(bb + B_OWN_POS, _I64), self._d(bb + B_OWN_SRC, _I64), self._d(bb + B_HOST_POS, _I64), host)
 
+    def peer_views(self, dev, j: int):
+        """(X0 positions, slots in rank j's buffer) of the rows rank j supplies, on the device
+        (views of the uploaded blob) — for staging.PeerDirect."""
+        self.device_blob(dev)
+        b = self._bb + BLOB_BATCH_SLOTS + 4 * j
+        return self._d(b, _I64), self._d(b + 2, _I64)
+
     def to_device(self, device, with_coo: bool = True, build: bool = True, graph=None):
         """The DeviceBatch of this batch: views of the uploaded blob (no further copies), then
         (build=True) the operand builds / GPU extractions on the current stream."""

@@ -19,14 +19,19 @@ Here (DESIGN.md §Feature staging):
     the critical path), then one contiguous hipMemcpyAsync on the side stream, then a scatter
     kernel into X0. Either way the side stream runs ahead, overlapping the previous batch's
     aggregation kernels; the compute stream waits on an event only when it needs X0.
-  * Peer rows (world_size > 1): exchanged with RCCL all-to-all (``PeerExchange``): the
-    request sizes and slot ids are negotiated on the host over a gloo group (no GPU sync),
-    each rank gathers the rows its peers asked for from its own buffer, one
-    all_to_all_single moves them over xGMI, and a scatter kernel places them.
+  * Peer rows (world_size > 1), two forms:
+    - ``PeerExchange`` (default): RCCL all-to-all — the request sizes and slot ids are
+      negotiated on the host over a gloo group (no GPU sync), each rank gathers the rows its
+      peers asked for from its own buffer, one all_to_all_single moves them over xGMI, and a
+      scatter kernel places them;
+    - ``PeerDirect`` (``--peer-rows direct``): every peer's buffer is mapped once (IPC) and the
+      staging stream's gather kernels read the batch's peer rows straight from the peers' HBM
+      over xGMI — no negotiation and no per-batch collective.
 """
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 import sys
 import weakref
@@ -340,6 +345,8 @@ class PeerExchange:
     kernel drops them at their X0 positions. Replaces the reference's per-peer P2P
     ``gpu_buffers[i][idx].to(device)`` copies (main.py:129-133)."""
 
+    needs_negotiation = True
+
     def __init__(self, group=None, meta_group=None):
         import torch.distributed as dist
 
@@ -386,3 +393,147 @@ class PeerExchange:
         if sum(sc):
             cso.gather_rows(recv_rows, None, x0, pos, n=sum(sc))
         return (want, pos, send_rows, recv_rows)
+
+
+def _ipc_close_all(mapped, device) -> None:
+    from . import _lib
+
+    with _lib.on_device(device):
+        for ptr, off in mapped:
+            _lib.lib().gnn_ipc_close(ptr, off)
+
+
+class PeerDirect:
+    """Peer rows read directly from the peers' feature buffers over xGMI.
+
+    Reference: main.py:129-133 copies ``gpu_buffers[i][idx]`` from every peer GPU by a P2P
+    ``.to(device)`` per batch. Here each rank maps every peer's buffer ONCE at start-up (an IPC
+    handle + offset per rank, exchanged by one all_gather_object on a gloo group,
+    ``gnn_ipc_export`` / ``gnn_ipc_open``) and a batch's peer rows are then gathered by HIP
+    kernels that read the peers' HBM straight into their X0 positions (one gnn_gather_rows_f32
+    per peer, on the staging stream). The slots come from the placement every rank computes
+    identically (``plan.peer_src``), so there is no per-batch negotiation and no collective:
+    ranks never wait for each other while staging. The buffers never change after start-up,
+    so no per-batch synchronisation with the peers is needed either. Same X0 as PeerExchange,
+    bit for bit (tests/test_dist_gpu.py)."""
+
+    needs_negotiation = False
+
+    def __init__(self, store: FeatureStore, group=None, feats: Optional[torch.Tensor] = None,
+                 buffer_nodes: Optional[list] = None):
+        """Collective (every rank of `group`). Raises on every rank if any rank could not map a
+        peer's buffer — all ranks agree before anyone raises, so none is left waiting. With
+        `feats` (the full feature table) and `buffer_nodes` (every rank's buffered node ids,
+        the placement's gpu_buffer_group), a few rows of every peer are read through the new
+        mapping and checked bit for bit before the first batch."""
+        import torch.distributed as dist
+        from . import _lib
+
+        self.dist = dist
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = dev = store.device
+        buf = store.gpu_buffer
+        self.ld = int(buf.stride(0))
+        self.peers = [None] * self.world  # (mapped pointer, rows, ld) per peer rank
+        mapped = []
+        self._closer = weakref.finalize(self, _ipc_close_all, mapped, dev)
+        with stdout_to_stderr():
+            self.group = dist.new_group(backend="gloo")
+        err, info = "", None
+        try:
+            if buf.shape[0]:
+                h = (ctypes.c_char * 64)()
+                off = ctypes.c_int64()
+                with _lib.on_device(dev):
+                    _lib.check(_lib.lib().gnn_ipc_export(buf.data_ptr(), h, ctypes.byref(off)), "gnn_ipc_export")
+                info = (bytes(h), int(off.value), dev.index, int(buf.shape[0]), self.ld)
+            torch.cuda.synchronize(dev)  # the buffer is final before any peer reads it
+        except Exception as e:  # noqa: BLE001 — reported to every rank below
+            err = f"rank {self.rank}: {e}"
+        infos = [None] * self.world
+        dist.all_gather_object(infos, (err, info), group=self.group)
+        err = "; ".join(e for e, _ in infos if e)
+        if not err:
+            try:
+                for j, (_, inf) in enumerate(infos):
+                    if j == self.rank or inf is None:
+                        continue
+                    handle, off, pdev, rows, ld = inf
+                    if ld != self.ld:
+                        raise RuntimeError(f"rank {j}'s buffer rows are {ld} floats, this rank's {self.ld}")
+                    ptr = ctypes.c_void_p()
+                    with _lib.on_device(dev):
+                        _lib.check(_lib.lib().gnn_ipc_open(handle, off, pdev if pdev != dev.index else -1,
+                                                           ctypes.byref(ptr)), "gnn_ipc_open")
+                    mapped.append((ptr.value, off))
+                    self.peers[j] = (ptr.value, rows, ld)
+                if feats is not None and buffer_nodes is not None:
+                    self._verify(feats, buffer_nodes)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {self.rank}: {e}"
+            errs = [None] * self.world
+            dist.all_gather_object(errs, err, group=self.group)
+            err = "; ".join(e for e in errs if e)
+        if err:
+            self._closer()
+            raise RuntimeError(f"PeerDirect unavailable: {err}")
+
+    def _verify(self, feats: torch.Tensor, buffer_nodes) -> None:
+        """Read the first, middle and last slot of every peer's buffer through the mapping and
+        compare with the feature table (catches a wrong offset or a mapping of the wrong GPU)."""
+        from . import _lib
+
+        dev, F = self.device, int(feats.shape[1])
+        for j, peer in enumerate(self.peers):
+            if peer is None:
+                continue
+            ptr, rows, ld = peer
+            slots = np.unique(np.array([0, rows // 2, rows - 1], np.int64))
+            src = torch.from_numpy(slots).to(dev)
+            out = torch.full((len(slots), ld), float("nan"), device=dev)
+            with _lib.on_device(dev):
+                _lib.check(_lib.lib().gnn_gather_rows_f32(ptr, ld, src.data_ptr(), out.data_ptr(), ld, None,
+                                                          len(slots), ld, _lib.stream_of(dev)), "gnn_gather_rows_f32")
+            got = out.cpu()
+            nodes = torch.from_numpy(np.asarray(buffer_nodes[j], np.int64)[slots])
+            if not torch.equal(got[:, :F], feats[nodes]):
+                raise RuntimeError(f"rows read from rank {j}'s mapped buffer differ from the feature table")
+
+    def prepare(self, plan: StagePlan):
+        return None
+
+    def close(self) -> None:
+        """Unmap the peers' buffers (after the last batch was staged; collective, so no rank
+        frees its buffer while a peer still has it mapped)."""
+        torch.cuda.synchronize(self.device)
+        self._closer()
+        self.dist.barrier(group=self.group)
+
+    def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore, meta=None):
+        from . import _lib
+
+        dev = x0.device
+        keep = []
+        for j in range(self.world):
+            n = len(plan.peer_src[j])
+            if j == self.rank or n == 0:
+                continue
+            peer = self.peers[j]
+            if peer is None:
+                raise RuntimeError(f"PeerDirect: the plan wants {n} rows from rank {j}, which buffers none")
+            ptr, rows, ld = peer
+            hi = int(np.max(plan.peer_src[j]))
+            if hi >= rows or int(np.min(plan.peer_src[j])) < 0:  # never read outside a peer's buffer
+                raise RuntimeError(f"PeerDirect: slot {hi} outside rank {j}'s buffer of {rows} rows")
+            if plan.blob is not None:
+                pos, src = plan.blob.peer_views(dev, j)
+            else:
+                pos = torch.from_numpy(np.ascontiguousarray(plan.peer_pos[j], np.int64)).to(dev, non_blocking=True)
+                src = torch.from_numpy(np.ascontiguousarray(plan.peer_src[j], np.int64)).to(dev, non_blocking=True)
+            keep += [pos, src]
+            with _lib.on_device(dev):
+                _lib.check(_lib.lib().gnn_gather_rows_f32(ptr, ld, src.data_ptr(), x0.data_ptr(), x0.stride(0),
+                                                          pos.data_ptr(), n, min(ld, x0.shape[1]),
+                                                          _lib.stream_of(dev)), "gnn_gather_rows_f32 (peer)")
+        return tuple(keep)

@@ -170,6 +170,18 @@ int gnn_gather_rows_host_f32(const float* host_src, int64_t ld_src, const int64_
 int gnn_host_register(void* host, size_t bytes);
 int gnn_host_unregister(void* host);
 
+/* Peer feature buffers read directly over xGMI (replaces the per-peer
+ * gpu_buffers[i][idx].to(device) P2P copies of main.py:129-133 without any per-step collective):
+ * each rank exports its buffer ONCE — an IPC handle of the allocation holding `ptr` and the byte
+ * offset of `ptr` in that allocation — the peers open it ONCE (peer access to `peer_device`
+ * enabled when it is another GPU), and gnn_gather_rows_f32 then reads a batch's peer rows
+ * straight from the mapped pointer into X0. The buffer must stay allocated and unchanged while
+ * peers hold it mapped; gnn_ipc_close undoes gnn_ipc_open. */
+#define GNN_IPC_HANDLE_BYTES 64
+int gnn_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out);
+int gnn_ipc_open(const void* handle, int64_t offset, int peer_device, void** ptr_out);
+int gnn_ipc_close(void* ptr, int64_t offset);
+
 /* One stream-ordered host-to-device copy (hipMemcpyAsync): the upload of a native loader's
  * batch blob (gnn_sampler.h) — every per-batch array of main.py:115-134 in one transfer. */
 int gnn_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);

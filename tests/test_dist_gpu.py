@@ -264,6 +264,74 @@ def _exchange_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
+def _direct_worker(rank, world, port, q):
+    """staging.PeerDirect: each rank maps the other's buffer once (IPC) and gathers the rows it
+    needs straight from it into X0 — same rows as the all-to-all exchange, bit for bit, and
+    nothing else in X0 touched."""
+    _env(rank, world, port)
+    import torch.distributed as dist
+
+    try:
+        from gnn_amd import staging
+        from gnn_amd.train import init_distributed
+
+        init_distributed()
+        dev = torch.device("cuda", 0)
+        F, k, n_in = 602, 300, 500
+        feats = torch.arange(world * k * F, dtype=torch.float32).view(world * k, F) * 1e-3
+        store = staging.FeatureStore(feats, np.arange(rank * k, (rank + 1) * k), dev, rank)
+        ex = staging.PeerDirect(store)
+        rng = np.random.default_rng(10 + rank)
+        empty = np.zeros(0, np.int64)
+        peer_pos, peer_src = [empty] * world, [empty] * world
+        perm = rng.permutation(n_in)
+        expect_rows, cut = [], 0
+        for j in range(world):
+            if j == rank:
+                continue
+            m = 120
+            peer_pos[j] = np.sort(perm[cut:cut + m]).astype(np.int64)
+            peer_src[j] = rng.integers(0, k, m).astype(np.int64)
+            peer_src[j][0] = k - 1  # the last slot of the peer's buffer
+            cut += m
+        plan = staging.StagePlan(n_in, empty, empty, empty, None, peer_pos, peer_src)
+        x0 = torch.full((n_in, store.ld), -1.0, device=dev)
+        st = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(st):
+            for _ in range(2):
+                ex.exchange(plan, x0, store)
+        torch.cuda.synchronize()
+        ok = True
+        got = x0.cpu()
+        for j in range(world):
+            if j == rank:
+                continue
+            want = torch.zeros((len(peer_src[j]), store.ld))
+            want[:, :F] = feats[torch.from_numpy(j * k + peer_src[j])]
+            ok = ok and torch.equal(got[torch.from_numpy(peer_pos[j])], want)
+        touched = np.concatenate([p for p in peer_pos if len(p)])
+        untouched = np.setdiff1d(np.arange(n_in), touched)
+        ok = ok and bool((got[torch.from_numpy(untouched)] == -1.0).all())
+        bad = False
+        try:  # a slot outside the peer's buffer is refused on the host, before any kernel
+            peer_src2 = list(peer_src)
+            peer_src2[1 - rank if world == 2 else (rank + 1) % world] = np.array([k], np.int64)
+            peer_pos2 = list(peer_pos)
+            peer_pos2[1 - rank if world == 2 else (rank + 1) % world] = np.array([0], np.int64)
+            ex.exchange(staging.StagePlan(n_in, empty, empty, empty, None, peer_pos2, peer_src2), x0, store)
+        except RuntimeError as e:
+            bad = "outside" in str(e)
+        ex.close()
+        q.put((rank, "ok" if ok and bad else f"rows differ or bound unchecked (rows ok {ok}, bound {bad})",
+               None, None))
+    except Exception as e:
+        q.put((rank, f"error: {e!r}", None, None))
+        raise
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
 def _spawn(fn, world=2, extra=()):
     import torch.multiprocessing as mp
 
@@ -375,3 +443,10 @@ def test_bucketed_exchange_world4():
     for rank, status, _, _ in out:
         assert status == "ok", f"rank {rank}: {status}"
     _check_against_reference(out, 4)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_direct_rows_bit_exact(world):
+    out = _spawn(_direct_worker, world=world)
+    for rank, status, _, _ in out:
+        assert status == "ok", f"rank {rank}: {status}"
