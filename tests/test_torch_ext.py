@@ -144,3 +144,35 @@ def test_torch_compile_traces_the_op(dev):
         outs.append((y.detach(), x.grad, w.grad))
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_module_in_the_reference_autograd_pattern(dev):
+    """The reference's SparseDenseMM (custom_sparse_ops.py:16-37) unchanged but for the module
+    object: forward spmm_load_balance(A, X), backward spmm_load_balance on A.transpose(0,1)
+    .coalesce() — a foreign coalesced COO the module has never seen (no cached CSR)."""
+    mod = torch_ops.load()
+
+    class RefSparseDenseMM(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, mat1, mat2):
+            ctx.save_for_backward(mat1)
+            return mod.spmm_load_balance(mat1, mat2)
+
+        @staticmethod
+        def backward(ctx, grad_output):
+            mat1, = ctx.saved_tensors
+            return None, mod.spmm_load_balance(mat1.transpose(0, 1).coalesce(), grad_output.contiguous())
+
+    full, rowptr, col, normfact, X, G = _case(4)
+    M, K = len(rowptr) - 1, X.shape[0]
+    t = lambda a: torch.from_numpy(a).to(dev)
+    A = mod.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int16)), t(normfact), M, K)
+    Xd = t(X).requires_grad_(True)
+    Y = RefSparseDenseMM.apply(A, Xd)
+    Y.backward(t(G))
+    torch.cuda.synchronize()
+    ocol, oval = O.build_operand(full, rowptr, col, normfact)
+    np.testing.assert_allclose(Y.detach().cpu().numpy(), O.spmm_f32(rowptr, ocol, oval, X), rtol=RTOL, atol=ATOL)
+    trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K)
+    np.testing.assert_allclose(Xd.grad.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
