@@ -497,6 +497,29 @@ def gather_ceiling(op, kernel_name, dev, reps=20, K=4096):
                     f"K = {K} rows (slice {K * 256 / 1e6:.1f} MB per XCD: cache-resident), median of {reps}"}
 
 
+def access_shape_ceiling(K, kernel_name):
+    """The aggregation's load stream with nothing else in it (scripts/gather_shape.hip, built by
+    build()): 64/G row pieces of G x 16 B per wave instruction, 4 in flight per lane group, 32
+    waves per CU, random rows of a K-row table with 608-float rows — at the dominant operand's
+    own K (the same slice per XCD) and cache-resident (K = 4096). A child process, run after the
+    timed passes; None if the probe is not built."""
+    import re
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "bin", "gather_shape")
+    m = re.match(r"spmm_unit_kernel<(\d+), (\d+), (\d+), (\d+)", kernel_name)
+    if m is None or not os.path.exists(exe):
+        return None
+    g, u = m.group(2), m.group(4)
+    out = {}
+    for tag, k in (("at_operand_K", int(K)), ("cache_resident", 4096)):
+        r = subprocess.run([exe, str(k), g, u], capture_output=True, text=True, timeout=120, check=True)
+        out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
+    out["what"] = ("scripts/gather_shape.hip: the dominant kernel's load stream alone (row pieces of G x 16 B, "
+                   "U in flight per lane group, 32 waves per CU, random rows), median of 20 launches")
+    return out
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -762,6 +785,12 @@ def main():
                 if ceil:
                     ceil["frac"] = round(roof["algorithmic"]["GBps"] / ceil["GBps"], 4)
                     roof["gather_ceiling"] = ceil
+                if world == 1:  # the probe runs on device 0 as a child process
+                    shape = access_shape_ceiling(step_batches[0][1].adjs[0].shape[1], dom)
+                    if shape:
+                        shape["frac_at_operand_K"] = round(
+                            roof["algorithmic"]["GBps"] / shape["at_operand_K"]["GBps"], 4)
+                        roof["access_shape"] = shape
             except Exception as e:  # a failed side measurement must not sink the benchmark
                 log(f"gather ceiling skipped: {e!r}")
         if args.cprofile and rank == 0:

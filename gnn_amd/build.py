@@ -1,5 +1,6 @@
 """In-tree builds: libgnn_spmm.so (hipcc, gfx950), libgnn_sampler.so (g++, host only) and the
-PyTorch-ROCm extension module `spmm` (g++ against torch + libgnn_spmm.so).
+PyTorch-ROCm extension module `spmm` (g++ against torch + libgnn_spmm.so), and the
+measurement probe scripts/bin/gather_shape (bench.py's access-shape ceiling).
 No JIT cache: the .so files live next to the package so they travel with the repository
 snapshot to the GPU box."""
 from __future__ import annotations
@@ -123,7 +124,34 @@ def build_torch_ext(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+PROBE_SRC = os.path.join(REPO, "scripts", "gather_shape.hip")
+PROBE_OUT = os.path.join(REPO, "scripts", "bin", "gather_shape")
+
+
+def build_probe(force: bool = False, verbose: bool = False) -> str:
+    """The access-shape microbenchmark bench.py runs for its live gather ceiling (a stand-alone
+    HIP program: the aggregation's load stream with nothing else in it)."""
+    with open(PROBE_SRC, "rb") as f:
+        bid = hashlib.sha1(f.read()).hexdigest()[:12]
+    stamp = PROBE_OUT + ".buildid"
+    if not force and os.path.exists(PROBE_OUT) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == bid:
+                return PROBE_OUT
+    os.makedirs(os.path.dirname(PROBE_OUT), exist_ok=True)
+    cmd = [os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"), f"--offload-arch={ARCH}", "-O3", "-std=c++17", PROBE_SRC,
+           "-o", PROBE_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(PROBE_OUT + ".tmp", PROBE_OUT)
+    with open(stamp, "w") as f:
+        f.write(bid)
+    return PROBE_OUT
+
+
 if __name__ == "__main__":
     print(build_library(force=True, verbose=True))
     print(build_sampler(force=True, verbose=True))
     print(build_torch_ext(force=True, verbose=True))
+    print(build_probe(force=True, verbose=True))

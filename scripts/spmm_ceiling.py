@@ -19,6 +19,7 @@ REPS launches, on operands with the REAL row lengths of a live-sampled Reddit LA
 
 Algorithmic bytes = nnz*F*4 + nnz*8 + (M+1)*4 + M*F*4 per launch.
 """
+import hashlib
 import json
 import os
 import sys
@@ -65,11 +66,19 @@ def main():
     def xmat(K, width=ld):
         return torch.randn(K, width, device=dev, generator=g)[:, :F]
 
-    for tag, op in (("real_L0", L0), ("real_L1", L1)):
-        X = xmat(op.shape[1])
-        ms, nb, kn, _ = timed(op, X, reps)
-        emit(case=tag, M=op.shape[0], K=op.shape[1], nnz=op.nnz, us=round(ms * 1e3, 1),
-             alg_GBps=round(nb / (ms * 1e-3) / 1e9, 1), kernel=kn, slice_MB=round(op.shape[1] * 256 / 1e6, 2))
+    # the step's own call shapes: layer-0 forward (F = 602 in 608-float rows), layer-1 forward and
+    # backward (F = 1024, the GraphSAGE hidden width); sha = checksum of the output bits (the
+    # prefetching and the plain kernel must agree bit for bit)
+    for tag, op, width in (("real_L0", L0, None), ("real_L1", L1, None), ("real_L1_F1024", L1, 1024),
+                           ("real_L1T_F1024", L1.transpose(), 1024)):
+        X = xmat(op.shape[1]) if width is None else torch.randn(op.shape[1], width, device=dev, generator=g)
+        ms, nb, kn, y = timed(op, X, reps)
+        sha = hashlib.md5(y.contiguous().cpu().numpy().tobytes()).hexdigest()[:16]
+        emit(case=tag, M=op.shape[0], K=op.shape[1], nnz=op.nnz, F=int(X.shape[1]), us=round(ms * 1e3, 1),
+             alg_GBps=round(nb / (ms * 1e-3) / 1e9, 1), kernel=kn, slice_MB=round(op.shape[1] * 256 / 1e6, 2),
+             sha=sha)
+    if os.environ.get("QUICK") == "1":
+        return
 
     # the layer-0 row lengths with uniform random columns over K rows of X
     rowptr = L0.rowptr
