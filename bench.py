@@ -26,6 +26,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -102,6 +103,8 @@ def parse():
     ap.add_argument("--peer-rows", default=os.environ.get("GNN_PEER_ROWS", "alltoall"), choices=["alltoall", "direct"],
                     help="N > 1: peer feature rows by an RCCL all-to-all per batch (default) or read directly "
                          "from the peers' buffers over xGMI (IPC-mapped once)")
+    ap.add_argument("--stage-ahead", type=int, default=int(os.environ.get("GNN_STAGE_AHEAD", "1")),
+                    help="batches whose X0 staging / device side are issued ahead of the current step")
     ap.add_argument("--numa", default="off", choices=["gpu", "off"],
                     help="confine the process (training + producer threads) to the CPUs of the GPU's NUMA node "
                          "(A/B on one box, 3 runs each: 572 vs 584 mini-batches/s unpinned, so off by default)")
@@ -597,17 +600,26 @@ def main():
 
     def _pipeline(next_item, steps):
         """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
-        needed + the operand builds). Batch i+1's X0 staging and batch_fn run on the side
-        stream, issued before batch i's step, so they overlap that step's kernels."""
+        needed + the operand builds). The X0 staging and batch_fn of batches i+1 .. i+A (A =
+        --stage-ahead) run on the side stream, issued before batch i's step, so they overlap
+        that step's kernels; with A = 2 a batch's staging has two steps' worth of the compute
+        stream's gaps to finish in (the compute kernels fill every CU, so staging kernels run
+        only in their gaps), and the compute stream does not wait for it between steps."""
         loss = None
-        staged = stager.issue(*next_item())
+        ahead = collections.deque()
+        issued = 0
+        while issued < min(args.stage_ahead, steps):
+            ahead.append(stager.issue(*next_item()))
+            issued += 1
         for i in range(steps):
-            staged_next = stager.issue(*next_item()) if i + 1 < steps else None
+            staged = ahead.popleft()
+            if issued < steps:
+                ahead.append(stager.issue(*next_item()))
+                issued += 1
             x0 = staged.wait(retire)
             db = staged.batch
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
-            staged = staged_next
         return loss
 
     def timed(fn_):
@@ -862,6 +874,7 @@ def main():
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "peer_rows": (args.peer_rows if world > 1 else None),
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
+                       "stage_ahead": args.stage_ahead,
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
                        "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host",
