@@ -516,10 +516,13 @@ def access_shape_ceiling(K, kernel_name):
     g, u = m.group(2), m.group(4)
     out = {}
     for tag, k in (("at_operand_K", int(K)), ("cache_resident", 4096)):
-        r = subprocess.run([exe, str(k), g, u], capture_output=True, text=True, timeout=120, check=True)
+        # long launches (1,024 row pieces per wave): the short default under-reads by the launch overhead
+        r = subprocess.run([exe, str(k), g, u], capture_output=True, text=True, timeout=120, check=True,
+                           env=dict(os.environ, PER_WAVE="1024"))
         out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
     out["what"] = ("scripts/gather_shape.hip: the dominant kernel's load stream alone (row pieces of G x 16 B, "
-                   "U in flight per lane group, 32 waves per CU, random rows), median of 20 launches")
+                   "U in flight per lane group, 32 waves per CU, random rows, 1,024 pieces per wave), median of "
+                   "20 launches")
     return out
 
 

@@ -37,7 +37,7 @@ constexpr int LD = 608;  // floats per X row (X0's padded stride)
 // Each wave owns `per_wave` consecutive row ids of `idx` (a multiple of 64). Per round a lane
 // loads one id; group g (lanes g*G .. g*G+G-1) then takes ids u * (64/G) + g for u < U' (U' = the
 // ids per round / (64/G)), issuing U loads before summing them.
-template <int G, int U>
+template <int G, int U, bool VAL = false>
 __global__ __launch_bounds__(256) void gather_kernel(const float4* __restrict__ X, const int* __restrict__ idx,
                                                      int per_wave, int tile4, float* __restrict__ out) {
   constexpr int GROUPS = 64 / G;
@@ -50,35 +50,38 @@ __global__ __launch_bounds__(256) void gather_kernel(const float4* __restrict__ 
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int base = 0; base < per_wave; base += PER_ROUND) {
     const int id = lane < PER_ROUND ? my[base + lane] : 0;
+    const float wv = VAL ? (float)(id & 7) * 0.25f : 1.0f;  // a per-piece value, as the operand's
     float4 v[U];
+    float w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = __shfl(id, u * GROUPS + grp);
+      w[u] = VAL ? __shfl(wv, u * GROUPS + grp) : 1.0f;
       v[u] = X[(int64_t)r * (LD / 4) + tile4 + gl];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc.x += v[u].x;
-      acc.y += v[u].y;
-      acc.z += v[u].z;
-      acc.w += v[u].w;
+      acc.x = __builtin_fmaf(w[u], v[u].x, acc.x);
+      acc.y = __builtin_fmaf(w[u], v[u].y, acc.y);
+      acc.z = __builtin_fmaf(w[u], v[u].z, acc.z);
+      acc.w = __builtin_fmaf(w[u], v[u].w, acc.w);
     }
   }
   out[wave * 64 + lane] = acc.x + acc.y + acc.z + acc.w;
 }
 
-template <int G, int U>
+template <int G, int U, bool VAL = false>
 double run(const float4* X, const int* idx, int waves, int per_wave, int tile4, float* out, int wpb) {
   const dim3 block(64 * wpb), grid(waves / wpb);
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  for (int w = 0; w < 3; ++w) gather_kernel<G, U><<<grid, block>>>(X, idx, per_wave, tile4, out);
+  for (int w = 0; w < 3; ++w) gather_kernel<G, U, VAL><<<grid, block>>>(X, idx, per_wave, tile4, out);
   CHECK(hipGetLastError());
   std::vector<float> ms;
   for (int rep = 0; rep < 20; ++rep) {
     CHECK(hipEventRecord(a));
-    gather_kernel<G, U><<<grid, block>>>(X, idx, per_wave, tile4, out);
+    gather_kernel<G, U, VAL><<<grid, block>>>(X, idx, per_wave, tile4, out);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float t = 0;
@@ -115,7 +118,8 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&X, hx.size() * sizeof(float)));
   CHECK(hipMemcpy(X, hx.data(), hx.size() * sizeof(float), hipMemcpyHostToDevice));
   // about 1.9 M row pieces per launch (the layer-0 operand's nonzero count)
-  const int per_wave = 256;
+  const char* pw = std::getenv("PER_WAVE");  // row pieces per wave (a multiple of 64): launch length
+  const int per_wave = pw ? std::max(64, atoi(pw) / 64 * 64) : 256;
   const int waves_per_cu = 32;
   const int waves = cus * waves_per_cu;  // one full round of the chip
   const int64_t rows = (int64_t)waves * per_wave;
@@ -132,10 +136,11 @@ int main(int argc, char** argv) {
     for (auto& v : hi) v = d(rng);
     CHECK(hipMemcpy(idx, hi.data(), rows * sizeof(int), hipMemcpyHostToDevice));
     double s = 0;
-    if (g == 32) s = run_u<32>(u, X, idx, waves, per_wave, out);
+    if (g == 8) s = run_u<8>(u, X, idx, waves, per_wave, out);
+    else if (g == 32) s = run_u<32>(u, X, idx, waves, per_wave, out);
     else if (g == 64) s = run_u<64>(u, X, idx, waves, per_wave, out);
     else s = run_u<16>(u, X, idx, waves, per_wave, out);
-    const int gg = (g == 32 || g == 64) ? g : 16;
+    const int gg = (g == 8 || g == 32 || g == 64) ? g : 16;
     std::printf("{\"K\": %lld, \"G\": %d, \"U\": %d, \"slice_MB\": %.2f, \"us\": %.1f, \"GBps\": %.1f}\n",
                 (long long)K, gg, u, K * gg * 16 / 1e6, s * 1e6, (double)rows * gg * 16 / s / 1e9);
     return 0;
@@ -148,9 +153,12 @@ int main(int argc, char** argv) {
     struct Case { int g, u, wpb; double s; };
     std::vector<Case> cs;
     cs.push_back({16, 4, 4, run<16, 4>(X, idx, waves, per_wave, 0, out, 4)});
+    cs.push_back({16, -4, 4, run<16, 4, true>(X, idx, waves, per_wave, 0, out, 4)});  // U = -4: + value shuffle, FMA
     cs.push_back({16, 2, 4, run<16, 2>(X, idx, waves, per_wave, 0, out, 4)});
     cs.push_back({16, 8, 4, run<16, 8>(X, idx, waves, per_wave, 0, out, 4)});
     cs.push_back({16, 16, 4, run<16, 16>(X, idx, waves, per_wave, 0, out, 4)});
+    cs.push_back({8, 4, 4, run<8, 4>(X, idx, waves, per_wave, 0, out, 4)});
+    cs.push_back({8, 8, 4, run<8, 8>(X, idx, waves, per_wave, 0, out, 4)});
     cs.push_back({32, 4, 4, run<32, 4>(X, idx, waves, per_wave, 0, out, 4)});
     cs.push_back({64, 4, 4, run<64, 4>(X, idx, waves, per_wave, 0, out, 4)});
     cs.push_back({64, 8, 4, run<64, 8>(X, idx, waves, per_wave, 0, out, 4)});
