@@ -31,12 +31,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gnn_amd import custom_sparse_ops as cso, graphs, placement, sampler as smp  # noqa: E402
 
 
-def timed(op, X, reps):
-    y = cso.spmm_csr(op, X)  # warm (and the output for checks)
+def timed(op, X, reps, unit=0):
+    y = cso.spmm_csr(op, X, unit_nnz=unit)  # warm (and the output for checks)
     cso.take_timing_records()
     cso.enable_timing(True)
     for _ in range(reps):
-        cso.spmm_csr(op, X)
+        cso.spmm_csr(op, X, unit_nnz=unit)
     recs = cso.take_timing_records()
     cso.enable_timing(False)
     ms = float(np.median([r[1] for r in recs]))
@@ -66,6 +66,11 @@ def main():
     def xmat(K, width=ld):
         return torch.randn(K, width, device=dev, generator=g)[:, :F]
 
+    # clocks up first: the first hundred-odd launches of a fresh process run slower
+    Xw = xmat(L0.shape[1])
+    for _ in range(int(os.environ.get("WARM", "100"))):
+        cso.spmm_csr(L0, Xw)
+    torch.cuda.synchronize()
     # the step's own call shapes: layer-0 forward (F = 602 in 608-float rows), layer-1 forward and
     # backward (F = 1024, the GraphSAGE hidden width); sha = checksum of the output bits (the
     # prefetching and the plain kernel must agree bit for bit)
@@ -77,6 +82,14 @@ def main():
         emit(case=tag, M=op.shape[0], K=op.shape[1], nnz=op.nnz, F=int(X.shape[1]), us=round(ms * 1e3, 1),
              alg_GBps=round(nb / (ms * 1e-3) / 1e9, 1), kernel=kn, slice_MB=round(op.shape[1] * 256 / 1e6, 2),
              sha=sha)
+    # work-unit size sweep on the step's call shapes (UNITS="256,512,..."): each wave's start-up
+    # (two row searches + the first (col, val) chunk) against its 16-64 rounds of gathers
+    for unit in [int(v) for v in os.environ.get("UNITS", "").split(",") if v]:
+        for tag, op, width in (("real_L0", L0, None), ("real_L1_F1024", L1, 1024),
+                               ("real_L1T_F1024", L1.transpose(), 1024)):
+            X = xmat(op.shape[1]) if width is None else torch.randn(op.shape[1], width, device=dev, generator=g)
+            ms, nb, kn, _ = timed(op, X, reps, unit)
+            emit(case=tag, unit=unit, us=round(ms * 1e3, 1), alg_GBps=round(nb / (ms * 1e-3) / 1e9, 1), kernel=kn)
     if os.environ.get("QUICK") == "1":
         return
 
