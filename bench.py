@@ -892,6 +892,7 @@ def main():
             "sampler": sampler_cost,
             "feature_staging": staging_info,
             "final_loss": round(final_loss, 5),
+            "peak_hbm_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
