@@ -205,3 +205,46 @@ def test_gpu_extraction_layer_mask(dev):
             for k in ("rowptr", "col", "val"):
                 assert torch.equal(getattr(a.transpose(), k), getattr(b.transpose(), k)), (li, "t", k)
     dd.graph.check()
+
+
+def _hub_graph():
+    """Two hub nodes adjacent to every node (rows of 30 k entries: segments spanning ~60 chunks
+    of the walk) on top of a sparse random graph, symmetric."""
+    rng = np.random.default_rng(21)
+    n = 30_000
+    u = rng.integers(0, n, 90_000)
+    v = rng.integers(0, n, 90_000)
+    hubs = np.array([0, 17])
+    hu = np.repeat(hubs, n)
+    hv = np.tile(np.arange(n), hubs.size)
+    r = np.concatenate([u, v, hu, hv])
+    c = np.concatenate([v, u, hv, hu])
+    keep = r != c
+    A = sp.csr_matrix((np.ones(keep.sum(), np.float32), (r[keep], c[keep])), shape=(n, n))
+    A.data[:] = 1
+    A.sort_indices()
+    return graphs.lap_matrix(A, "graphsage")
+
+
+@pytest.mark.gpu
+def test_gpu_extraction_hub_rows(dev):
+    """Rows far longer than a walk chunk (the hubs' 30 k-entry rows, in U and in lapᵀ): the
+    device-extracted operands and transposes equal the host path's, bit for bit."""
+    lap = _hub_graph()
+    N = lap.shape[0]
+    batch = np.concatenate([[0, 17], np.random.default_rng(4).choice(np.arange(18, N), 254, replace=False)])
+    args = (29, batch, np.array([3000] * 5), N, lap, _labels(N), [1, 1, 1], np.full(N, -1), np.zeros(N, np.int64),
+            None, 1.0, [0])
+    hb = sampler.ladies_sample_host(*args)
+    hd = sampler.ladies_sample_host(*args, device_extract=True)
+    assert any(L is not None and L.on_device for L in hd.layers)
+    db = hb.to_device(dev, with_coo=False)
+    dd = hd.to_device(dev, with_coo=False)
+    torch.cuda.synchronize()
+    for li, (a, b) in enumerate(zip(db.adjs, dd.adjs)):
+        for k in ("rowptr", "col", "val"):
+            assert torch.equal(getattr(a, k), getattr(b, k)), (li, k)
+        if li >= 1:
+            for k in ("rowptr", "col", "val"):
+                assert torch.equal(getattr(a.transpose(), k), getattr(b.transpose(), k)), (li, "t", k)
+    dd.graph.check()
