@@ -12,14 +12,15 @@ instead into the two halves of a ring all-reduce, with the reduction moved after
      (GNN_SH_GRAD_EVENTS, include/gnn_step.h): an all-to-all on a side stream sends shard j of
      this rank's UNSCALED bucket to rank j — while the layers below are still in their
      backward on the compute stream (RCCL over xGMI beside the compute kernels). The LAST
-     bucket (layer 0, final when the backward ends) travels after the clip factor is known,
-     with the factor appended to every shard (one collective for both);
+     bucket (layer 0, final when the backward ends) travels after the backward, straight from
+     the flat gradient, and the ranks' clip factors by one all-gather of W floats;
   2. per bucket: rank r sums its shard over the ranks in rank order, Σ_j c_j * g_j[shard r]
      (each product rounded in fp32 as the reference's clip-then-add);
   3. ONE all-to-all returns every rank's summed shards of every bucket (an all-gather with
      unequal shards), and one copy puts them into the flat gradient, which Adam reads.
-So two collectives follow the backward (the flat path: one all-reduce of the whole gradient),
-and the reduce-scatter half of the traffic of the other buckets is off the critical path.
+So three collectives follow the backward, two of them tiny or small (the flat path: one
+all-reduce of the whole gradient), and the reduce-scatter half of the traffic of the other
+buckets is off the critical path.
 Buckets = backward stages: [head + top layer], [layer L-2], ..., [layer 0].
 """
 from __future__ import annotations
@@ -63,11 +64,8 @@ class BucketedExchange:
             n = hi - lo
             self.sz.append([n // W + (1 if j < n % W else 0) for j in range(W)])
         self.off = [[sum(s[:j]) for j in range(W)] for s in self.sz]
-        self.recv = [torch.empty(W * s[r], dtype=torch.float32, device=dev) for s in self.sz[:-1]]
-        # the last bucket travels with the clip factor appended to each shard
-        last = self.sz[-1]
-        self.last_send = torch.empty(sum(last) + W, dtype=torch.float32, device=dev)
-        self.last_recv = torch.empty(W * (last[r] + 1), dtype=torch.float32, device=dev)
+        self.recv = [torch.empty(W * s[r], dtype=torch.float32, device=dev) for s in self.sz]
+        self.fac = torch.empty(W, dtype=torch.float32, device=dev)  # every rank's clip factor
         # the gather phase: this rank's summed shards of every bucket, one copy per destination
         self.mine = sum(s[r] for s in self.sz)
         self.red = torch.empty(self.mine, dtype=torch.float32, device=dev)
@@ -113,24 +111,18 @@ class BucketedExchange:
             c = self.opt.scale
         else:
             c = torch.ones(1, dtype=torch.float32, device=self.device)
+        dist.all_gather_into_tensor(self.fac, c.view(1), group=self.group)
+        fac = self.fac.view(W, 1)  # c_j of every rank
         lo, hi = self.buckets[-1]
-        last, lof = self.sz[-1], self.off[-1]
-        for j in range(W):  # [shard j | c_r] for each destination j
-            o = lof[j] + j
-            self.last_send[o:o + last[j]].copy_(flat[lo + lof[j]:lo + lof[j] + last[j]])
-            self.last_send[o + last[j]:o + last[j] + 1].copy_(c)
-        dist.all_to_all_single(self.last_recv, self.last_send, output_split_sizes=[last[r] + 1] * W,
-                               input_split_sizes=[s + 1 for s in last], group=self.group)
-        lr = self.last_recv.view(W, last[r] + 1)
-        fac = lr[:, last[r]:].contiguous()  # c_j of every rank, (W, 1)
+        dist.all_to_all_single(self.recv[-1], flat[lo:hi], output_split_sizes=[self.sz[-1][r]] * W,
+                               input_split_sizes=self.sz[-1], group=self.group)
         for w in self.works:
             w.wait()  # the current stream waits for the side stream's all-to-alls
         torch.cuda.current_stream(self.device).wait_stream(self.stream)
         o = 0
         for b in range(len(self.buckets)):
             q = self.sz[b][r]
-            src = self.recv[b].view(W, q) if b < len(self.buckets) - 1 else lr[:, :q]
-            torch.sum(src * fac, dim=0, out=self.red[o:o + q])
+            torch.sum(self.recv[b].view(W, q) * fac, dim=0, out=self.red[o:o + q])
             o += q
         self.gsend.view(W, self.mine).copy_(self.red.view(1, self.mine).expand(W, self.mine))
         dist.all_to_all_single(self.grecv, self.gsend, output_split_sizes=self.gsizes,
