@@ -157,8 +157,10 @@ struct WorkMap {
   }
 };
 
+// One column chunk per lane: held to 8 waves per SIMD (<= 64 VGPRs; the slot-skip branches
+// below otherwise take 66); wider instantiations keep the compiler's choice (no spills).
 template <int VW, int G, int NJ, int U, bool RES>
-__global__ __launch_bounds__(256) void spmm_unit_kernel(
+__global__ __launch_bounds__(256, NJ == 1 ? 8 : 1) void spmm_unit_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
     int M, int nnz, int S, int nunits,
     const float* __restrict__ X, int64_t ldx,
@@ -262,6 +264,14 @@ __global__ __launch_bounds__(256) void spmm_unit_kernel(
           }
           vs[t] = v;
           const float* xr = X + (int64_t)c * ldx;
+          // a slot past the row end for every lane group (the row's last, partly empty round:
+          // 6-7 % of the slots on the Reddit layers) issues no load; its FMA adds 0 * 0, as the
+          // loaded-and-masked slot added 0 * x: bit-identical (A/B: layer-0 forward -1 %)
+          if (k + t * P >= n) {  // wave-uniform
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) xs[t][j] = vzero<VW>();
+            continue;
+          }
           // Columns past F load the row's last vector instead (same cache lines, no
           // branch, no extra HBM bytes); those accumulator slots are never stored.
 #pragma unroll
