@@ -4,13 +4,14 @@ Reference: per-rank threads in one process; grads flattened with torch.cat, publ
 shared list, ``threading.Barrier``, summed with P2P ``.to(device)`` copies (main.py:149-168);
 per-rank clip_grad_norm_(5) BEFORE the sum and no averaging (main.py:146,159).
 
-Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). With the
-native step executor the exchange is bucketed per backward stage and overlapped with the
-backward (gnn_amd.dp: all-to-all of unscaled shards as each stage finishes, then this rank's
-clip factor, the weighted shard sums and an all-gather — the same per-rank-clip-then-sum).
-Otherwise the per-rank clip writes the clipped gradients straight into one flat fp32 buffer
-(one kernel, gnn_amd.optim), summed with ONE in-place ``all_reduce(SUM)``, and Adam reads them
-as views of that buffer; at N = 1 the clip factor is applied inside the Adam launch. (On the CPU
+Here: one process per GPU with torch.distributed (backend "nccl" = RCCL over xGMI). By default
+the per-rank clip writes the clipped gradients straight into one flat fp32 buffer (one kernel,
+gnn_amd.optim), summed with ONE in-place ``all_reduce(SUM)``, and Adam reads them as views of
+that buffer; at N = 1 the clip factor is applied inside the Adam launch. With the native step
+executor and GNN_DP_BUCKETS=1 the exchange is bucketed per backward stage and overlapped with
+the backward instead (gnn_amd.dp: all-to-all of unscaled shards as each stage finishes, then
+the ranks' clip factors, the weighted shard sums and one gather — the same
+per-rank-clip-then-sum, bit-identical at world 2); bench.py times both at N > 1. (On the CPU
 — the gloo tests — the same semantics run through torch's clip_grad_norm_ and Adam.)
 Gradients are reset to None each step, so autograd hands its freshly computed tensors over
 instead of accumulating into old ones. Initial weights are broadcast from rank 0 (the
