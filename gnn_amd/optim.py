@@ -10,7 +10,7 @@ them from there.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional
+from typing import List
 
 import torch
 
