@@ -27,10 +27,10 @@
 //  * The kept entries leave compacted (ballot + mbcnt) into a GAPPED buffer at the chunk's own
 //    entry position (a chunk keeps at most its range), with the chunk's count; A's row pointer
 //    gets, for each segment starting in the chunk, the kept entries of the chunk before it.
-//  * The last chunk to finish in each group of 64 publishes the group's total (an agent-scope
-//    counter, write-through count words); a compaction pass (a wave per chunk: its prefix from
-//    the lower chunks of its group + the lower groups' totals, coalesced copies of its entries to
-//    that prefix, rowptr += prefix) finishes.
+//  * Every chunk adds its count to its group's total (groups of 64 chunks; one agent-scope add,
+//    nothing awaited); a compaction pass (a wave per chunk: its prefix from the lower chunks of
+//    its group + the lower groups' totals, coalesced copies of its entries to that prefix,
+//    rowptr += prefix) finishes.
 //    Measured on the Reddit layer 0 (13 M graph entries with the transpose): a single walk that
 //    waited for the lower chunks' counts (chained or two-level prefix) spent ~45 % of its time
 //    waiting — every wave of a launch ends its walk at about the same time — while the gapped
@@ -113,8 +113,8 @@ struct Side {
   int* qs;                     // [xw+1] first segment starting at or after each chunk's start (prep)
   unsigned long long* gap;     // [T] kept entries (index | value bits << 32) at their chunk's entry position
   int* cnt;                    // [xw] kept entries per chunk
-  int* gcnt;                   // [xw / GROUP] arrivals per group of chunks (zeroed by prep)
-  int* gsum;                   // [xw / GROUP] kept entries per group (its last arriving chunk)
+  int* gcnt;                   // [xw / GROUP] arrivals per group of chunks (zeroed by prep; GSUM = false)
+  int* gsum;                   // [xw / GROUP] kept entries per group (zeroed by prep)
   int* rowptr;                 // A: the output row pointer [R+1]; Aᵀ: NULL (host colptr)
   int* out_idx;                // col (A) / rows_t (Aᵀ)
   float* out_val;
@@ -186,6 +186,7 @@ __global__ __launch_bounds__(256) void lx_prep_kernel(Sides sd) {
     const int ng = (s.xw + GROUP - 1) / GROUP;
     if (i < ng) {
       s.gcnt[i] = 0;
+      s.gsum[i] = 0;
       return;
     }
     i -= ng;
@@ -231,7 +232,7 @@ __device__ __forceinline__ void chunk_segments(const Side& s, int w, int a, int&
 }
 
 // One chunk w of side s by one wave (see the file comment).
-template <int XU, bool LDS>
+template <int XU, bool LDS, bool GSUM>
 __device__ __forceinline__ void walk_chunk(const Side& s, int w, int lane, const Word* ltab,
                                            const int* __restrict__ degree, const float* __restrict__ normfact) {
   const int T = s.T;
@@ -291,30 +292,51 @@ __device__ __forceinline__ void walk_chunk(const Side& s, int w, int lane, const
 #pragma unroll
     for (int t = 0; t < XU; ++t) val[t] = (float)((1.0 / (double)(m[t] >= 0 ? aux[t] : 1)) * (double)nf[t]);
   }
-  // 4. the kept entries, compacted into the gapped buffer at the chunk's entry position; the count
+  // 4. the chunk's count, then its kept entries compacted into the gapped buffer at the chunk's
+  //    entry position
   unsigned long long km[XU];
   int total = 0;
 #pragma unroll
   for (int t = 0; t < XU; ++t) {
     km[t] = __ballot(m[t] >= 0);
-    const int pos = a + total + below_me(km[t]);
-    if (m[t] >= 0) G(s.gap)[pos] = (unsigned)m[t] | ((unsigned long long)__float_as_uint(val[t]) << 32);
     total += __builtin_popcountll(km[t]);
   }
-  // the count, and the group's total by the group's last arriving chunk (MI355X_MICROARCH.md,
-  // Valid forms, table row 1: sc1 count stores drained before the agent-scope counter add; the
-  // last adder reads the counts with sc1 loads after its add returned)
-  if (lane == 0) __hip_atomic_store(G(s.cnt) + w, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int g = w / GROUP, gsize = min(GROUP, s.xw - g * GROUP);
-  int last = 0;
-  if (lane == 0)
-    last = __hip_atomic_fetch_add(G(s.gcnt) + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
-  if (__builtin_amdgcn_readfirstlane(last)) {
-    const int c = lane < gsize ? __hip_atomic_load(G(s.cnt) + g * GROUP + lane, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) : 0;
-    const int gs = wave_sum(c);
-    if (lane == 0) G(s.gsum)[g] = gs;
+  const int g = w / GROUP;
+  if constexpr (GSUM) {
+    // the group's total by one agent-scope add per chunk, no returned value awaited: nothing in
+    // this launch reads it (the compaction, a later launch, does), so no wave waits for its stores
+    // or for another wave (round 3, late; was: count stores drained, then an arrival counter whose
+    // last adder summed the group's counts)
+    if (lane == 0) {
+      G(s.cnt)[w] = total;
+      __hip_atomic_fetch_add(G(s.gsum) + g, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  {
+    int run = 0;
+#pragma unroll
+    for (int t = 0; t < XU; ++t) {
+      const int pos = a + run + below_me(km[t]);
+      if (m[t] >= 0) G(s.gap)[pos] = (unsigned)m[t] | ((unsigned long long)__float_as_uint(val[t]) << 32);
+      run += __builtin_popcountll(km[t]);
+    }
+  }
+  if constexpr (!GSUM) {
+    // the count, and the group's total by the group's last arriving chunk (MI355X_MICROARCH.md,
+    // Valid forms, table row 1: sc1 count stores drained before the agent-scope counter add; the
+    // last adder reads the counts with sc1 loads after its add returned)
+    if (lane == 0) __hip_atomic_store(G(s.cnt) + w, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int gsize = min(GROUP, s.xw - g * GROUP);
+    int last = 0;
+    if (lane == 0)
+      last = __hip_atomic_fetch_add(G(s.gcnt) + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+    if (__builtin_amdgcn_readfirstlane(last)) {
+      const int c = lane < gsize ? __hip_atomic_load(G(s.cnt) + g * GROUP + lane, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) : 0;
+      const int gs = wave_sum(c);
+      if (lane == 0) G(s.gsum)[g] = gs;
+    }
   }
   // 5. A: for the segments starting in this range (the last chunk: up to R), the kept entries of
   //    the range before them (the compaction adds the chunk's prefix)
@@ -339,7 +361,7 @@ __device__ __forceinline__ void walk_chunk(const Side& s, int w, int lane, const
 
 // A workgroup of WGW waves walks WGW * CPW consecutive chunks of one side (each wave CPW of them,
 // one after the other), sharing one LDS copy of the membership table in LDS mode.
-template <int XU, int WGW, int CPW, bool LDS>
+template <int XU, int WGW, int CPW, bool LDS, bool GSUM>
 __global__ __launch_bounds__(64 * WGW, XU == 8 ? 8 : 4) void lx_walk_kernel(Sides sd, const int* __restrict__ degree,
                                                            const float* __restrict__ normfact) {
   extern __shared__ __attribute__((aligned(16))) Word ltab[];
@@ -361,7 +383,7 @@ __global__ __launch_bounds__(64 * WGW, XU == 8 ? 8 : 4) void lx_walk_kernel(Side
 #pragma unroll 1
   for (int c = 0; c < CPW; ++c) {
     const int w = w0 + c * WGW + wave;
-    if (w < s.xw) walk_chunk<XU, LDS>(s, w, lane, ltab, degree, normfact);
+    if (w < s.xw) walk_chunk<XU, LDS, GSUM>(s, w, lane, ltab, degree, normfact);
   }
 }
 
@@ -529,14 +551,18 @@ int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, const 
   const int wgw = lds ? LDS_WAVES : GLB_WAVES, cpw = lds ? LDS_CPW : 1;
   const dim3 grid((unsigned)(waves / (wgw * cpw))), block((unsigned)(64 * wgw));
   const size_t shm = lds ? tab_bytes : 0;
-  if (XU == 8 && lds)
-    lx_walk_kernel<8, LDS_WAVES, LDS_CPW, true><<<grid, block, shm, st>>>(sd, degree, normfact);
+  bool gsum = true;  // GNN_LX_GSUM=0: the last-arriver group sums (A/B)
+  if (const char* e = getenv("GNN_LX_GSUM")) gsum = atoi(e) != 0;
+  if (XU == 8 && lds && gsum)
+    lx_walk_kernel<8, LDS_WAVES, LDS_CPW, true, true><<<grid, block, shm, st>>>(sd, degree, normfact);
+  else if (XU == 8 && lds)
+    lx_walk_kernel<8, LDS_WAVES, LDS_CPW, true, false><<<grid, block, shm, st>>>(sd, degree, normfact);
   else if (XU == 8)
-    lx_walk_kernel<8, GLB_WAVES, 1, false><<<grid, block, 0, st>>>(sd, degree, normfact);
+    lx_walk_kernel<8, GLB_WAVES, 1, false, true><<<grid, block, 0, st>>>(sd, degree, normfact);
   else if (lds)
-    lx_walk_kernel<16, LDS_WAVES, LDS_CPW, true><<<grid, block, shm, st>>>(sd, degree, normfact);
+    lx_walk_kernel<16, LDS_WAVES, LDS_CPW, true, true><<<grid, block, shm, st>>>(sd, degree, normfact);
   else
-    lx_walk_kernel<16, GLB_WAVES, 1, false><<<grid, block, 0, st>>>(sd, degree, normfact);
+    lx_walk_kernel<16, GLB_WAVES, 1, false, true><<<grid, block, 0, st>>>(sd, degree, normfact);
   GNN_LAUNCHED("lx_walk_kernel");
   int ccpw = COMPACT_CPW;
   if (const char* e = getenv("GNN_LX_CCPW")) ccpw = atoi(e);
