@@ -325,23 +325,26 @@ __global__ __launch_bounds__(256, NJ == 1 ? 8 : 1) void spmm_unit_kernel(
 }
 
 // Adds the unit pieces of every cut row (> S nonzeros), in unit order. A workgroup covers
-// 16 rows: every wave loads their rowptr pairs at once (one dependent round, not one per
-// row) and ballots the cut ones; the (cut row, 64*VW-column pass) items are dealt to the 4
-// waves, so a cluster of long rows still spreads over the workgroup.
+// `rows` rows (<= 64): every wave loads their rowptr pairs at once (one dependent round, not one
+// per row) and ballots the cut ones; the (cut row, 64*VW-column pass) items are dealt to the 4
+// waves, so a cluster of long rows still spreads over the workgroup. 16 rows per workgroup, fewer
+// for small operands (the layer-2 forward: 512 rows, most of them cut, 4 column passes each —
+// 32 workgroups dealt each wave ~8 items in a row).
 constexpr int COMBINE_ROWS = 16;
+int combine_rows(int64_t M) { return M >= 2048 ? COMBINE_ROWS : (M >= 512 ? 4 : 1); }
 
 template <int VW>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int* __restrict__ rowptr, int M, int S,
     const float* __restrict__ slab, int64_t ldslab,
     float* __restrict__ Y, int64_t ldy, int F,
-    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
+    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap, int rows) {
   using V = typename Vec<VW>::T;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int r0 = blockIdx.x * COMBINE_ROWS;
+  const int r0 = blockIdx.x * rows;
   const int rl = r0 + lane;
-  const bool is_cut = lane < COMBINE_ROWS && rl < M && (rowptr[rl + 1] - rowptr[rl]) > S;  // ownership rule
+  const bool is_cut = lane < rows && rl < M && (rowptr[rl + 1] - rowptr[rl]) > S;  // ownership rule
   const unsigned long long cutmask = __ballot(is_cut);
   if (cutmask == 0ull) return;
   const int npass = (F + 64 * VW - 1) / (64 * VW);
@@ -1388,19 +1391,21 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
   GNN_LAUNCHED("spmm_unit_kernel");
   if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
-    const dim3 g2((unsigned)ceil_div(M, (int64_t)COMBINE_ROWS));
+    int crows = combine_rows(M);
+    if (const char* e = getenv("GNN_SPMM_CROWS")) crows = std::min(64, std::max(1, atoi(e)));  // A/B
+    const dim3 g2((unsigned)ceil_div(M, (int64_t)crows));
     switch (c.vw) {
       case 4:
         spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap);
+                                                         R, ldr, (const int*)rmap, crows);
         break;
       case 2:
         spmm_combine_kernel<2><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap);
+                                                         R, ldr, (const int*)rmap, crows);
         break;
       default:
         spmm_combine_kernel<1><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap);
+                                                         R, ldr, (const int*)rmap, crows);
         break;
     }
     GNN_LAUNCHED("spmm_combine_kernel");
