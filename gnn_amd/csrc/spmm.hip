@@ -331,9 +331,10 @@ __global__ __launch_bounds__(256, NJ == 1 ? 8 : 1) void spmm_unit_kernel(
 // for small operands (the layer-2 forward: 512 rows, most of them cut, 4 column passes each —
 // 32 workgroups dealt each wave ~8 items in a row).
 constexpr int COMBINE_ROWS = 16;
+constexpr int COMBINE_LOADS = 4;  // pieces of a cut row loaded before they are added
 int combine_rows(int64_t M) { return M >= 2048 ? COMBINE_ROWS : (M >= 512 ? 4 : 1); }
 
-template <int VW>
+template <int VW, int COMBINE_BATCH>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int* __restrict__ rowptr, int M, int S,
     const float* __restrict__ slab, int64_t ldslab,
@@ -361,19 +362,24 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
     const int u1 = (re - 1) / S;
     const int q = rmap ? rmap[r] : -1;
     {
-      V s = *reinterpret_cast<const V*>(slab + ((int64_t)u0 * 2 + 1) * ldslab + cc);
-      int u = u0 + 1;
-      for (; u + 4 <= u1 + 1; u += 4) {
-        const V a0 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 0) * 2) * ldslab + cc);
-        const V a1 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 1) * 2) * ldslab + cc);
-        const V a2 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 2) * 2) * ldslab + cc);
-        const V a3 = *reinterpret_cast<const V*>(slab + ((int64_t)(u + 3) * 2) * ldslab + cc);
-        s += a0;
-        s += a1;
-        s += a2;
-        s += a3;
+      // pieces in unit order: slot 1 of u0, then slot 0 of u0 + 1 .. u1, added in that order,
+      // COMBINE_BATCH pieces' loads in flight at once (A/B of 2 / 4 / 8 / 16 under the bench,
+      // profiles/round3/spmm/combine_loads_r3ar_r3as/: 4 and 8 equal, 2 and 16 slower)
+      const int np = u1 - u0 + 1;  // wave-uniform
+      V s = vzero<VW>();
+      for (int b = 0; b < np; b += COMBINE_BATCH) {
+        V a[COMBINE_BATCH];
+#pragma unroll
+        for (int k = 0; k < COMBINE_BATCH; ++k) {
+          const int p = b + k;
+          if (p < np) a[k] = *reinterpret_cast<const V*>(slab + ((int64_t)(u0 + p) * 2 + (p == 0 ? 1 : 0)) * ldslab + cc);
+        }
+#pragma unroll
+        for (int k = 0; k < COMBINE_BATCH; ++k) {
+          const int p = b + k;
+          if (p < np) s = p == 0 ? a[k] : s + a[k];
+        }
       }
-      for (; u <= u1; ++u) s += *reinterpret_cast<const V*>(slab + ((int64_t)u * 2) * ldslab + cc);
       if (q >= 0) s += *reinterpret_cast<const V*>(R + (int64_t)q * ldr + cc);
       *reinterpret_cast<V*>(Y + (int64_t)r * ldy + cc) = s;
     }
@@ -1394,20 +1400,13 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
     int crows = combine_rows(M);
     if (const char* e = getenv("GNN_SPMM_CROWS")) crows = std::min(64, std::max(1, atoi(e)));  // A/B
     const dim3 g2((unsigned)ceil_div(M, (int64_t)crows));
-    switch (c.vw) {
-      case 4:
-        spmm_combine_kernel<4><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap, crows);
-        break;
-      case 2:
-        spmm_combine_kernel<2><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap, crows);
-        break;
-      default:
-        spmm_combine_kernel<1><<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F,
-                                                         R, ldr, (const int*)rmap, crows);
-        break;
-    }
+    auto combine = [&](auto kern) {
+      kern<<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F, R, ldr,
+                                     (const int*)rmap, crows);
+    };
+    if (c.vw == 4) combine(spmm_combine_kernel<4, COMBINE_LOADS>);
+    else if (c.vw == 2) combine(spmm_combine_kernel<2, COMBINE_LOADS>);
+    else combine(spmm_combine_kernel<1, COMBINE_LOADS>);
     GNN_LAUNCHED("spmm_combine_kernel");
   }
   return 0;

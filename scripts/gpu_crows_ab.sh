@@ -1,5 +1,7 @@
-# Rows per combine workgroup: default (16, 4 for the 512-row layer-2 forward) vs 16 everywhere,
-# A/B/A/B under rocprofv3 kernel traces of the default bench (300 steps); the SpMM GPU tests first.
+# Combine-kernel A/Bs under rocprofv3 kernel traces of the default bench (300 steps), the SpMM GPU
+# tests first. Arguments: one env setting per run ("-" = defaults), e.g. "-" "GNN_SPMM_CROWS=16"
+# (rows per combine workgroup) or "GNN_SPMM_CBATCH=4" (pieces per load round); none = the round-3
+# rows-per-workgroup A/B/A/B.
 set -o pipefail
 TAG=${TAG:-cr}
 mkdir -p gpurun_out/cr_$TAG
@@ -8,9 +10,10 @@ REPO=$(pwd)
 timeout -k 10 300 python -u -m pytest tests/test_spmm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/cr_$TAG/tests.log 2>&1 || { echo "tests failed"; exit 1; }
 i=0
-for v in default 16 default 16; do
+[ $# -eq 0 ] && set -- - GNN_SPMM_CROWS=16 - GNN_SPMM_CROWS=16
+for E in "$@"; do
   i=$((i+1))
-  if [ "$v" = "default" ]; then E=""; else E="GNN_SPMM_CROWS=$v"; fi
+  v=${E#*=}; [ "$E" = "-" ] && { E=""; v=default; }
   (cd /tmp && env $E timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d /tmp/cr_$i -o run -- \
       python -u $REPO/bench.py --steps 300 --no-cpu-baseline --no-traffic --no-roofline \
       > $REPO/gpurun_out/cr_$TAG/bench_${i}_$v.json 2> $REPO/gpurun_out/cr_$TAG/bench_${i}_$v.err) || exit 1
