@@ -327,12 +327,13 @@ __global__ __launch_bounds__(256, NJ == 1 ? 8 : 1) void spmm_unit_kernel(
 // Adds the unit pieces of every cut row (> S nonzeros), in unit order. A workgroup covers
 // `rows` rows (<= 64): every wave loads their rowptr pairs at once (one dependent round, not one
 // per row) and ballots the cut ones; the (cut row, 64*VW-column pass) items are dealt to the 4
-// waves, so a cluster of long rows still spreads over the workgroup. 16 rows per workgroup, fewer
-// for small operands (the layer-2 forward: 512 rows, most of them cut, 4 column passes each —
-// 32 workgroups dealt each wave ~8 items in a row).
-constexpr int COMBINE_ROWS = 16;
+// waves, so a cluster of long rows still spreads over the workgroup. 4 rows per workgroup (1 for
+// operands under 512 rows): more, smaller workgroups finish sooner beside the concurrent staging
+// kernels — combines per step 50.9 (16 rows) vs 45.4 (4 rows) vs 71.9 (32) us, and the layer-2
+// forward's 10.7 -> 6.0 us (A/B/A/B under the bench, profiles/round3/spmm/combine_rows_*).
+constexpr int COMBINE_ROWS = 4;
 constexpr int COMBINE_LOADS = 4;  // pieces of a cut row loaded before they are added
-int combine_rows(int64_t M) { return M >= 2048 ? COMBINE_ROWS : (M >= 512 ? 4 : 1); }
+int combine_rows(int64_t M) { return M >= 512 ? COMBINE_ROWS : 1; }
 
 template <int VW, int COMBINE_BATCH>
 __global__ __launch_bounds__(256) void spmm_combine_kernel(
