@@ -20,8 +20,10 @@ Synthetic Reddit-shaped graph: Chung-Lu lognormal sigma 1.3, N 
 `--cpu`: BASELINE config 1 (samp 512, batch 128, one process on the CPU through the product's
 torch.sparse.mm device branch).
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run.
-Rank 0 prints ONE JSON line.
+Run: python bench.py [--gpus N --steps K --warmup W]. For N > 1 the command starts its own N rank
+processes (gnn_amd.launch, before any GPU call; as the reference's one `python main.py` starts a
+trainer per device, main.py:289-297) unless a launcher (torch.distributed.run) already set
+WORLD_SIZE. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -39,7 +41,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from gnn_amd import custom_sparse_ops as cso  # noqa: E402
-from gnn_amd import graphs, placement, sampler, staging  # noqa: E402
+from gnn_amd import graphs, launch, placement, sampler, staging  # noqa: E402
 from gnn_amd.models import build_model  # noqa: E402
 from gnn_amd.train import Trainer, init_distributed  # noqa: E402
 
@@ -112,6 +114,13 @@ def parse():
     ap.add_argument("--python-loader", action="store_true",
                     help="batch producer: Python worker threads calling the native sampler (BatchLoader) instead of "
                          "the C++ producer (NativeLoader: GIL-free workers, one blob and one H2D per batch)")
+    ap.add_argument("--locality-sampling", action="store_true",
+                    help="the reference's --locality_sampling (main.py:284-287): per-layer skewed node sets from the "
+                         "placement (preprocess.py:414-423) handed to the sampler; at the reference's scale_factor "
+                         "1.0 (main.py:256) they leave the draw unchanged (sampler.py:119-121)")
+    ap.add_argument("--scale-factor", type=float, default=1.0,
+                    help="sampler.py:119-121's boost of the skewed nodes' probability (the reference fixes 1.0); "
+                         "> 1 takes the numpy restatement in Python producer threads")
     ap.add_argument("--cprofile", default="", help="after the timed runs, cProfile 20 GPU steps into this file")
     ap.add_argument("--dump-batch", default="", help="save rank-0 batch 0 operands (.npz) for kernel profiling")
     a = ap.parse_args()
@@ -318,6 +327,8 @@ def workload_name(args, spec) -> str:
     model = "GraphSAGE" if args.model == "graphsage" else "GCN"
     smp = args.sampler.upper() if args.sampler != "fastgcn" else "FastGCN"
     w = f"{GRAPH_NAMES[args.graph]} {model} {smp} samp_num={args.samp_num} batch_size={args.batch_size}"
+    if getattr(args, "locality_sampling", False):
+        w += f" + locality_sampling (scale_factor {args.scale_factor:g})"
     if args.graph == "reddit" and (args.model, args.sampler) == ("graphsage", "ladies"):
         if (args.samp_num, args.batch_size) == (8192, 512) and not args.cpu:
             w += " (BASELINE config 2)"
@@ -441,6 +452,10 @@ def roofline_from(recs, step_batches, args, traffic, steps):
         "algorithmic": {"GB_per_launch": round(alg / 1e9, 4), "GBps": round(alg / t / 1e9, 1),
                         "what": "SURVEY.md §8(d): every gathered X row counted (re-reads served by L2 / Infinity "
                                 "Cache), no fraction: it is not an HBM quantity"},
+        # the same launches against the three bases side by side (frac above: PMC L2-egress / HBM peak)
+        "frac_alg_8d": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+        "frac_alg_8d_what": "SURVEY.md §8(d) algorithmic bytes (every gathered X row, L2 hits included) / "
+                            "launch duration / 8 TB/s HBM peak: above 1 because re-reads are served by L2",
         "l2_gather": {"ceiling_GBps": L2_GATHER_PEAK_GBS, "frac": round(alg / t / 1e9 / L2_GATHER_PEAK_GBS, 4),
                       "what": "algorithmic gather rate / the L2-served row-gather rate of MI355X_MICROARCH.md "
                               "§Indexed rows (18.8 TB/s chip-wide)"},
@@ -530,6 +545,21 @@ def access_shape_ceiling(K, kernel_name):
 # ----------------------------------------------------------------------------- main
 def main():
     args = parse()
+    if not args.cpu and launch.needs_launch(args.gpus):
+        # one command starts every rank (no external torchrun needed); nothing above touched the GPU
+        sys.exit(launch.relaunch_self(args.gpus))
+    held = {}
+    try:
+        _main(args, held)
+    except BaseException:
+        # a failing rank unmaps its peers' buffers (after a device sync) without the collective
+        # close(): the peers may never reach its barrier (the launcher stops them instead)
+        if held.get("direct") is not None:
+            held["direct"].close_local()
+        raise
+
+
+def _main(args, held):
     spec = {"reddit": graphs.REDDIT, "products": graphs.PRODUCTS, "papers": graphs.PAPERS_SCALED,
             "tiny": graphs.TINY}[args.graph]
     t0 = time.time()
@@ -553,8 +583,18 @@ def main():
     log(f"placement k={k} per GPU ({time.time() - t0:.1f}s)")
     samp = np.array([args.samp_num] * 5)
     fn = SAMPLERS[args.sampler]
+    skewed = None
+    if args.locality_sampling:  # main.py:284-287: on graph_data[0] + I, every rank's buffer
+        import scipy.sparse as sp
+
+        skewed = placement.get_skewed_sampled_nodes(A + sp.eye(N, dtype=A.dtype, format="csr"), pl.gpu_buffer_group,
+                                                    [1, 1, 1])
+        log(f"locality sampling: skewed node sets {[len(s) for s in skewed]} ({time.time() - t0:.1f}s)")
+    if args.scale_factor > 1 and not args.python_loader:
+        log("scale_factor > 1: the numpy restatement in Python producer threads (--python-loader)")
+        args.python_loader = True
     probe_batch = fn(99, sampler.rank_batches(train, args.batch_size, rank, world, 0)[0], samp, N, lap, labels,
-                     [1, 1, 1], pdev, pidx, None, 1.0, list(range(world)))
+                     [1, 1, 1], pdev, pidx, skewed, args.scale_factor, list(range(world)))
     traffic = None
     if rank == 0 and world == 1 and not args.no_traffic and not args.no_roofline:
         # before this process initialises the GPU: the probes are child processes
@@ -569,16 +609,26 @@ def main():
 
     store = staging.FeatureStore(feats, pl.gpu_buffer_group[rank], dev, rank, zero_copy=args.staging == "zerocopy")
     exchange = direct = alltoall = None
+    peer_info = None
     if world > 1:
         alltoall = staging.PeerExchange()
+        requested, direct_err = args.peer_rows, None
         if args.peer_rows == "direct" or os.environ.get("GNN_BENCH_PEER_AB", "1") == "1":
             try:  # collective; every rank gets the same outcome
                 direct = staging.PeerDirect(store, feats=feats, buffer_nodes=pl.gpu_buffer_group)
             except RuntimeError as e:
+                direct_err = str(e)
                 log(f"{e} -> peer rows by all-to-all")
+        held["direct"] = direct
         if args.peer_rows == "direct" and direct is None:
             args.peer_rows = "alltoall"
         exchange = direct if args.peer_rows == "direct" else alltoall
+        peer_info = {"requested": requested, "used": args.peer_rows, "direct_mapped": direct is not None,
+                     "direct_verified_rows": direct.verified_rows if direct is not None else 0,
+                     "direct_error": direct_err[:400] if direct_err else None,
+                     "what": "peer-row form of the reported passes after PeerDirect's all-or-nothing set-up "
+                             "(direct_verified_rows: rows read through this rank's IPC mappings of the peers' "
+                             "buffers and found bit-equal to the feature table before the first batch)"}
     stager = staging.Stager(store, exchange)
     torch.manual_seed(0)
     model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
@@ -661,7 +711,8 @@ def main():
         lkw["device_count"] = dev
     loader = (BatchLoader if args.python_loader else NativeLoader)(
         lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank, world_size=world,
-        store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx, **lkw)
+        store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx,
+        skewed_sampling_nodes=skewed, scale_factor=args.scale_factor, **lkw)
     if dx:  # the graph resident in HBM for the extraction (made once, outside every timed region)
         sampler.device_graph(loader.graph, dev)
         torch.cuda.synchronize()
@@ -825,6 +876,7 @@ def main():
                         shape["frac_at_operand_K"] = round(
                             roof["algorithmic"]["GBps"] / shape["at_operand_K"]["GBps"], 4)
                         roof["access_shape"] = shape
+                        roof["frac_access_shape"] = shape["frac_at_operand_K"]
             except Exception as e:  # a failed side measurement must not sink the benchmark
                 log(f"gather ceiling skipped: {e!r}")
         if args.cprofile and rank == 0:
@@ -846,8 +898,14 @@ def main():
         if isinstance(it, staging.NegotiatedStream):
             it.close()
     final_loss = float(loss.item()) if loss is not None else float("nan")
+    # every rank must end with bit-identical parameters (summed gradient + the same Adam update,
+    # main.py:146-170): the N > 1 line carries its own consistency proof (collective)
+    agree = trainer.check_ranks_agree()
+    if not agree["identical"]:
+        log(f"PARAMETERS DIFFER ACROSS RANKS: {agree['digests']}")
     if direct is not None:
         direct.close()  # every rank's staging is done before any buffer is unmapped / freed
+        held["direct"] = None
     if dx:  # every GPU extraction of the run agreed with the host's counts (syncs; outside the timings)
         sampler.device_graph(loader.graph, dev).check()
 
@@ -897,6 +955,7 @@ def main():
                        "peer_rows": (args.peer_rows if world > 1 else None),
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
                        "stage_ahead": args.stage_ahead,
+                       "locality_sampling": args.locality_sampling, "scale_factor": args.scale_factor,
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
                        "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host",
@@ -911,12 +970,17 @@ def main():
             "sampler": sampler_cost,
             "feature_staging": staging_info,
             "final_loss": round(final_loss, 5),
+            "ranks": {"params_identical_across_ranks": agree["identical"], "param_digests": agree["digests"],
+                      "peer_rows": peer_info,
+                      "what": "sha256 of every rank's parameters after all passes, all-gathered"},
             "peak_hbm_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    if not agree["identical"]:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

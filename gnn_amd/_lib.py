@@ -34,6 +34,7 @@ _SIGNATURES = {
     "gnn_spmm_csr_f32": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _SZ, _I64, _VP]),
     "gnn_spmm_csr_f32_ex": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _I64, _VP,
                                    _VP, _SZ, _I64, _VP]),
+    "gnn_spmm_kernel_name": (_INT, [_I64, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, _INT, ctypes.c_char_p, _SZ]),
     "gnn_spmm_config":(_INT, [_I64, _I64, _I64, _I64, _I64, _I64, _VP, _VP, _I64, ctypes.POINTER(ctypes.c_int32)]),
     "gnn_spmm_set_timing_events": (None, [_VP, _VP]),
     "gnn_segsort_workspace_bytes": (_SZ, [_I64]),

@@ -388,6 +388,107 @@ __global__ __launch_bounds__(256) void spmm_combine_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// Small operands (the layer-2 calls: 15 k nonzeros, F = 1024): one workgroup of WPR waves per
+// (row, column slice of 64 * VW * NJ floats), no work units, no slab, no combine launch.
+// The unit kernel's parallelism comes from many equal units; on a 15 k-entry operand it has a
+// few thousand short waves, each a chain of dependent loads (row search, (col, val), gathers
+// in rounds of U, store) with 4 row loads in flight: 24-25 us per call + a combine launch for
+// the cut rows, latency-bound. Here a wave owns one row (WPR = 1) or a contiguous 1/WPR of it
+// (long rows: the layer-2 forward's 512 rows reach 484 nonzeros), issues U row loads per lane
+// before its FMAs, and the WPR partial rows are added in wave order through LDS by wave 0.
+// WPR = 1: every output element is a C fmaf chain over the row in CSR order (bit-identical to
+// the oracle); WPR > 1: WPR such chains added in order (deterministic). Empty rows store zeros
+// (or the residual row).
+// ---------------------------------------------------------------------------------
+template <int VW, int NJ, int U, int WPR, bool RES>
+__global__ __launch_bounds__(64 * WPR) void spmm_row_kernel(
+    const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val, int M,
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int F, int slices,
+    const float* __restrict__ R, int64_t ldr, const int* __restrict__ rmap) {
+  using V = typename Vec<VW>::T;
+  constexpr int COVER = 64 * VW * NJ;
+  __shared__ V part[WPR > 1 ? WPR - 1 : 1][NJ][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int r = (int)(blockIdx.x / (unsigned)slices);
+  const int s = (int)(blockIdx.x - (unsigned)r * (unsigned)slices);
+  if (r >= M) return;
+  const int c0 = s * COVER + lane * VW;
+  int q = -1;
+  if constexpr (RES) q = rmap[r];  // issued early: its latency overlaps the walk
+  const int rb = rowptr[r];
+  const int re = rowptr[r + 1];
+  const int per = (re - rb + WPR - 1) / WPR;
+  const int b = rb + w * per;
+  const int e = min(re, b + per);
+  V acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = vzero<VW>();
+  for (int base = b; base < e; base += 64) {
+    const int n = min(64, e - base);
+    int mc = 0;
+    float mv = 0.0f;
+    if (lane < n) {
+      mc = col[base + lane];
+      mv = val[base + lane];
+    }
+    for (int k = 0; k < n; k += U) {
+      V xs[U][NJ];
+      float vs[U];
+#pragma unroll
+      for (int t = 0; t < U; ++t) {
+        const int idx = k + t;  // wave-uniform
+        if (idx >= n) {        // past the chunk: no load, the FMA adds 0 * 0
+          vs[t] = 0.0f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) xs[t][j] = vzero<VW>();
+          continue;
+        }
+        const int c = readlane_i(mc, idx);  // scalar row address
+        vs[t] = readlane_f(mv, idx);
+        const float* xr = X + (int64_t)c * ldx;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int cc = min(c0 + j * 64 * VW, F - VW);  // past F: the row's last vector (unstored)
+          xs[t][j] = *reinterpret_cast<const V*>(xr + cc);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // all U * NJ row loads ahead of the FMAs
+#pragma unroll
+      for (int t = 0; t < U; ++t) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[j] = vfma(vs[t], xs[t][j], acc[j]);
+      }
+    }
+  }
+  if constexpr (WPR > 1) {
+    if (w > 0) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) part[w - 1][j][lane] = acc[j];
+    }
+    __syncthreads();
+    if (w > 0) return;
+#pragma unroll
+    for (int p = 0; p < WPR - 1; ++p) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[j] += part[p][j][lane];
+    }
+  }
+  float* dst = Y + (int64_t)r * ldy;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int cc = c0 + j * 64 * VW;
+    if (cc < F) {
+      V a = acc[j];
+      if constexpr (RES) {
+        if (q >= 0) a += *reinterpret_cast<const V*>(R + (int64_t)q * ldr + cc);
+      }
+      *reinterpret_cast<V*>(dst + cc) = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Operand builder: value = (float)((1.0 / full_degree(row)) * (double)normfact[col]),
 // the formula of cuda_spmm.cu:800 evaluated in double. A flat nnz-balanced pass builds
 // every entry; rows found out of column order (never from a scipy-sliced sub-graph, but a
@@ -1090,7 +1191,41 @@ __global__ __launch_bounds__(256) void gather_rows_host_kernel(const float* __re
 struct SpmmCfg {
   int vw, g, nj, tiles;
   int64_t unit, nunits, ldslab;
+  // small operands: spmm_row_kernel<vw, rnj, ru, wpr> over M * slices workgroups (wpr == 0: the
+  // unit kernel above)
+  int wpr, rnj, ru, slices;
 };
+
+// The row kernel takes operands whose nonzeros are too few to fill the chip with units: up to
+// ROWK_MAX_NNZ nonzeros and ROWK_MAX_WG workgroups (GNN_SPMM_ROWK=0 / 1 forces it off / on when
+// the caller did not fix the unit size).
+constexpr int64_t ROWK_MAX_NNZ = 65536;
+constexpr int64_t ROWK_MAX_WG = 1 << 20;
+
+void pick_row_kernel(SpmmCfg& c, int64_t M, int64_t nnz, int64_t F, int64_t unit) {
+  c.wpr = 0;
+  if (unit > 0 || M <= 0 || F <= 0) return;  // a fixed unit size asks for the unit kernel
+  const char* env = getenv("GNN_SPMM_ROWK");
+  const int mode = env ? atoi(env) : -1;
+  if (mode == 0) return;
+  const int64_t chunks = ceil_div(F, (int64_t)64 * c.vw);  // 64-lane column chunks covering F
+  // many rows: whole rows per wave, up to 4 chunks per lane; few rows: one chunk per slice
+  int nj = 1;
+  if (c.vw == 4 && M >= 4096) nj = chunks >= 4 ? 4 : (chunks >= 2 ? 2 : 1);
+  const int64_t slices = ceil_div(chunks, (int64_t)nj);
+  const double avg = (double)nnz / (double)M;
+  int wpr = avg >= 48.0 ? 8 : (avg >= 12.0 ? 4 : 1);
+  if (const char* e = getenv("GNN_SPMM_ROWK_WPR")) {  // experiments
+    const int v = atoi(e);
+    if (v == 1 || v == 2 || v == 4 || v == 8) wpr = v;
+  }
+  if (mode != 1 && (nnz > ROWK_MAX_NNZ || M * slices > ROWK_MAX_WG)) return;
+  if (M * slices >= (int64_t)INT_MAX) return;
+  c.wpr = wpr;
+  c.rnj = nj;
+  c.ru = nj == 1 ? 16 : (nj == 2 ? 8 : 4);
+  c.slices = (int)slices;
+}
 
 int pick_vw(int64_t F, int64_t ldx, int64_t ldy, const void* X, const void* Y) {
   const uintptr_t px = (uintptr_t)X, py = (uintptr_t)Y;
@@ -1203,6 +1338,7 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
   c.unit = unit > 0 ? unit : default_unit(M, nnz, F);
   c.nunits = nnz > 0 ? ceil_div(nnz, c.unit) : 1;
   c.ldslab = (int64_t)align_up((size_t)(F > 0 ? F : 1), 4);
+  pick_row_kernel(c, M, nnz, F, unit);
   return c;
 }
 
@@ -1266,6 +1402,41 @@ MainFn select_main(const SpmmCfg& c, bool res) {
     case 1: return main_by_g<1>(c.g, c.nj, res);
     default: return nullptr;
   }
+}
+
+using RowFn = void (*)(const int*, const int*, const float*, int, const float*, int64_t, float*, int64_t, int, int,
+                      const float*, int64_t, const int*);
+
+template <int VW, int NJ, int U>
+RowFn row_by_wpr(int wpr, bool res) {
+  switch (wpr) {
+    case 1: return res ? &spmm_row_kernel<VW, NJ, U, 1, true> : &spmm_row_kernel<VW, NJ, U, 1, false>;
+    case 2: return res ? &spmm_row_kernel<VW, NJ, U, 2, true> : &spmm_row_kernel<VW, NJ, U, 2, false>;
+    case 4: return res ? &spmm_row_kernel<VW, NJ, U, 4, true> : &spmm_row_kernel<VW, NJ, U, 4, false>;
+    case 8: return res ? &spmm_row_kernel<VW, NJ, U, 8, true> : &spmm_row_kernel<VW, NJ, U, 8, false>;
+    default: return nullptr;
+  }
+}
+
+RowFn select_row(const SpmmCfg& c, bool res) {
+  if (c.vw == 4) {
+    if (c.rnj == 4) return row_by_wpr<4, 4, 4>(c.wpr, res);
+    if (c.rnj == 2) return row_by_wpr<4, 2, 8>(c.wpr, res);
+    return row_by_wpr<4, 1, 16>(c.wpr, res);
+  }
+  if (c.rnj != 1) return nullptr;
+  if (c.vw == 2) return row_by_wpr<2, 1, 16>(c.wpr, res);
+  return row_by_wpr<1, 1, 16>(c.wpr, res);
+}
+
+// The main kernel's name as rocprofv3 lists it (bench.py's per-kernel roofline).
+std::string main_kernel_name(const SpmmCfg& c, bool res) {
+  char b[96];
+  if (c.wpr)
+    snprintf(b, sizeof b, "spmm_row_kernel<%d, %d, %d, %d, %s>", c.vw, c.rnj, c.ru, c.wpr, res ? "true" : "false");
+  else
+    snprintf(b, sizeof b, "spmm_unit_kernel<%d, %d, %d, %d, %s>", c.vw, c.g, c.nj, pick_u(c.nj), res ? "true" : "false");
+  return b;
 }
 
 void tr_tiles(int64_t nnz, int64_t& TS, int64_t& T) {
@@ -1332,7 +1503,17 @@ int64_t gnn_spmm_default_unit_nnz(int64_t M, int64_t nnz, int64_t F) { return de
 
 size_t gnn_spmm_workspace_bytes(int64_t M, int64_t nnz, int64_t F, int64_t unit_nnz) {
   const SpmmCfg c = make_cfg(M, 0, nnz, F, F, F, nullptr, nullptr, unit_nnz);
+  // (the row kernel needs none; the size stays the unit kernel's, which a call with other
+  // strides / alignment may take)
   return align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
+}
+
+int gnn_spmm_kernel_name(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+                         const void* Y, int64_t unit_nnz, int residual, char* out, size_t out_bytes) {
+  GNN_REQUIRE(out != nullptr && out_bytes > 0, "gnn_spmm_kernel_name: out is NULL");
+  const std::string n = main_kernel_name(make_cfg(M, K, nnz, F, ldx, ldy, X, Y, unit_nnz), residual != 0);
+  snprintf(out, out_bytes, "%s", n.c_str());
+  return 0;
 }
 
 int gnn_spmm_config(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
@@ -1375,6 +1556,19 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
   GNN_REQUIRE(nnz == 0 || (col && val && X), "gnn_spmm_csr_f32: NULL col/val/X");
   GNN_REQUIRE(rmap == nullptr || (R != nullptr && F <= ldr), "gnn_spmm_csr_f32_ex: rmap needs R with F <= ldr");
   const SpmmCfg c = make_cfg(M, K, nnz, F, ldx, ldy, X, Y, unit_nnz);
+  hipStream_t st = (hipStream_t)stream;
+  if (c.wpr) {  // small operand: one workgroup per (row, column slice), nothing to combine
+    GNN_REQUIRE(rmap == nullptr || (ldr % c.vw == 0 && (uintptr_t)R % (4 * c.vw) == 0),
+                "gnn_spmm_csr_f32_ex: R (ldr %lld) not aligned for %d-wide vectors", (long long)ldr, c.vw);
+    RowFn fn = select_row(c, rmap != nullptr);
+    GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no row kernel for vw=%d nj=%d wpr=%d", c.vw, c.rnj, c.wpr);
+    if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
+    hipLaunchKernelGGL(fn, dim3((unsigned)(M * c.slices)), dim3(64 * c.wpr), 0, st, rowptr, col, val, (int)M, X, ldx,
+                       Y, ldy, (int)F, c.slices, R, ldr, (const int*)rmap);
+    GNN_LAUNCHED("spmm_row_kernel");
+    if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
+    return 0;
+  }
   GNN_REQUIRE(c.nunits * c.unit < (int64_t)INT_MAX + c.unit, "gnn_spmm_csr_f32: unit overflow");
   GNN_REQUIRE(c.nunits <= (int64_t)INT_MAX / 2, "gnn_spmm_csr_f32: too many units");
   const size_t need = align_up((size_t)c.nunits * 2 * (size_t)c.ldslab * sizeof(float), 256);
@@ -1386,7 +1580,6 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
               "gnn_spmm_csr_f32_ex: R (ldr %lld) not aligned for %d-wide vectors", (long long)ldr, c.vw);
   MainFn fn = select_main(c, rmap != nullptr);
   GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no kernel for vw=%d g=%d nj=%d", c.vw, c.g, c.nj);
-  hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
   GNN_REQUIRE(ceil_div(c.nunits + ceil_div(M, (int64_t)ROW_UNIT), 4) * c.tiles < (int64_t)INT_MAX - 8,
               "gnn_spmm_csr_f32: grid too large");

@@ -141,6 +141,11 @@ at::Tensor create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& row
                                  idx.data_ptr<int64_t>(), ws.data_ptr(), wsb, current_stream(ci)),
            "gnn_build_operand_f32");
   at::Tensor out = at::_sparse_coo_tensor_unsafe(idx, val, {nrows, ncols}, nf.options());
+  // Columns come out ascending per row; a repeated (row, col) pair (never made by the reference's
+  // samplers) is summed as the reference's .coalesce() does (cuda_spmm.cu:825), so a tensor
+  // flagged coalesced really is (one small check, synchronising as the reference's coalesce does).
+  if (nnz > 1 && at::eq(idx.narrow(1, 1, nnz - 1), idx.narrow(1, 0, nnz - 1)).all(0).any().item<bool>())
+    return out.coalesce();
   return out._coalesced_(true);
 }
 

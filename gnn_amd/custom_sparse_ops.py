@@ -53,7 +53,8 @@ def enable_timing(flag: bool = True) -> None:
 
 def take_timing_records(sync: bool = True):
     """Return [(tag, ms, algorithmic_bytes, kernel_name, dims)] for recorded calls and clear
-    the list (kernel_name as rocprofv3 lists the main kernel: spmm_unit_kernel<VW, G, NJ, U>;
+    the list (kernel_name as rocprofv3 lists the main kernel: spmm_unit_kernel<VW, G, NJ, U, RES> or,
+    small operands, spmm_row_kernel<VW, NJ, U, WPR, RES>;
     dims = {M, K, nnz, F, res_rows}: the call's shape, residual rows read if any).
 
     Also folds the times into spmm_forward_time / spmm_backward_time (seconds)."""
@@ -80,14 +81,13 @@ def record_timing(tag, e0, e1, M, K, nnz, F, Fk, ldx, ldy, xptr, yptr, unit_nnz,
     """Append one timed aggregation launch (events e0 / e1 armed around its main kernel) — also
     used by the native step executor, whose launches are armed from C (gnn_amd.executor)."""
     L = _lib.lib()
-    cfg = (ctypes.c_int32 * 6)()
-    L.gnn_spmm_config(M, K, nnz, Fk, ldx, ldy, xptr, yptr, unit_nnz, cfg)
-    u = 4 if cfg[2] <= 4 else (3 if cfg[2] == 5 else 2)  # pick_u (spmm.hip)
+    name = ctypes.create_string_buffer(128)
+    _lib.check(L.gnn_spmm_kernel_name(M, K, nnz, Fk, ldx, ldy, xptr, yptr, unit_nnz, int(bool(residual)), name, 128),
+               "gnn_spmm_kernel_name")
     nbytes = algorithmic_bytes(M, nnz, F)
     if residual:  # residual rows read + the row map
         nbytes += res_rows * F * 4 + M * 4
-    res = "true" if residual else "false"
-    _timing_records.append((tag, e0, e1, nbytes, f"spmm_unit_kernel<{cfg[0]}, {cfg[1]}, {cfg[2]}, {u}, {res}>",
+    _timing_records.append((tag, e0, e1, nbytes, name.value.decode(),
                             dict(M=M, K=K, nnz=nnz, F=F, res_rows=res_rows if residual else 0)))
 
 
@@ -452,6 +452,11 @@ def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> tor
     if all(isinstance(t, torch.Tensor) and t.device.type == "cpu" for t in ins):
         return _create_coo_tensor_cpu(*ins, int(nrows), int(ncols))
     op, coo = build_operand(fullrowptr, rowptr, colidx, normfact, int(nrows), int(ncols), with_coo=True)
+    if coo.shape[1] > 1 and bool(((coo[:, 1:] == coo[:, :-1]).all(0)).any()):
+        # a repeated column within a row (the reference's samplers never make one: LADIES' after
+        # nodes are unique, sampler.py:135-139): sum the duplicates as the reference's .coalesce()
+        # does (cuda_spmm.cu:825); the CSR image is then rebuilt from the coalesced tensor
+        return torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols))).coalesce()
     t = torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols)), is_coalesced=True)
     t._gnn_csr = op
     return t
@@ -525,4 +530,8 @@ def spmm_config(M: int, nnz: int, F: int, ldx: Optional[int] = None, ldy: Option
     out = (ctypes.c_int32 * 6)()
     _lib.check(_lib.lib().gnn_spmm_config(M, K, nnz, F, ldx or F, ldy or F, 256, 256, unit_nnz, out),
                "gnn_spmm_config")
-    return dict(vw=out[0], g=out[1], nj=out[2], tiles=out[3], unit_nnz=out[4], units=out[5])
+    name = ctypes.create_string_buffer(128)
+    _lib.check(_lib.lib().gnn_spmm_kernel_name(M, K, nnz, F, ldx or F, ldy or F, 256, 256, unit_nnz, 0, name, 128),
+               "gnn_spmm_kernel_name")
+    return dict(vw=out[0], g=out[1], nj=out[2], tiles=out[3], unit_nnz=out[4], units=out[5],
+                kernel=name.value.decode())

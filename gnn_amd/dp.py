@@ -57,6 +57,13 @@ class BucketedExchange:
             if sum(offs[i][1] - offs[i][0] for i in idx) != hi - lo:
                 raise ValueError("BucketedExchange: a backward stage's gradients are not contiguous in the flat buffer")
             self.buckets.append((lo, hi))
+        # the buckets must tile the whole flat gradient: finish() writes back only the bucket
+        # positions, so an element outside every bucket would keep this rank's unclipped local
+        # gradient and the ranks would silently diverge (the Trainer then uses the flat exchange)
+        cover = sorted(self.buckets)
+        if (not cover or cover[0][0] != 0 or cover[-1][1] != flat.numel()
+                or any(a[1] != b[0] for a, b in zip(cover, cover[1:]))):
+            raise ValueError(f"BucketedExchange: buckets {cover} do not tile the flat gradient [0, {flat.numel()})")
         W, r = self.world, self.rank
         # shard j of bucket b: [lo + off_b[j], lo + off_b[j] + sz_b[j])
         self.sz = []

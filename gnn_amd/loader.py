@@ -79,7 +79,13 @@ class BatchLoader:
     def __init__(self, lap, labels_full, train_nodes, samp_num: int, batch_size: int, orders: Sequence[int],
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
-                 seed: int = 0, devices=None, kind: str = "ladies", device_extract=False):
+                 seed: int = 0, devices=None, kind: str = "ladies", device_extract=False,
+                 skewed_sampling_nodes=None, scale_factor: float = 1.0):
+        """skewed_sampling_nodes / scale_factor: --locality_sampling (main.py:284-287,
+        preprocess.py:414-423), passed to every sampler call as the reference's prepare_data does
+        (sampler.py:163-193); they change the LADIES draw only when scale_factor > 1
+        (sampler.py:119-121; the reference fixes scale_factor = 1.0, main.py:256), which takes
+        the numpy restatement."""
         fns = {"ladies": smp.ladies_sample_host, "subgraph": smp.subgraph_sample_host,
                "fastgcn": smp.fastgcn_sample_host}
         if kind not in fns:
@@ -103,11 +109,13 @@ class BatchLoader:
         self.workers = max(1, int(workers))
         self.prefetch = prefetch if prefetch > 0 else 2 * self.workers
         self.rng = np.random.RandomState(seed + 7919 * rank)
+        self.skewed = skewed_sampling_nodes
+        self.scale_factor = float(scale_factor)
         self.pool = ThreadPoolExecutor(max_workers=self.workers, thread_name_prefix="gnn-sampler")
 
     def _produce(self, seed: int, nodes: np.ndarray) -> LoadedBatch:
         hb = self.sample_fn(seed, nodes, self.samp, self.graph.num_nodes, self.graph, self.labels, self.orders,
-                            self.dev_of, self.idx_on, None, 1.0, self.devices, **self.kw)
+                            self.dev_of, self.idx_on, self.skewed, self.scale_factor, self.devices, **self.kw)
         hb.pin()
         plan = staging.make_plan(hb, self.store, self.rank, self.world, self.devices) if self.store else None
         return LoadedBatch(hb, plan)
@@ -361,9 +369,17 @@ class NativeLoader:
                  device_id_of_nodes, idx_of_nodes_on_device, rank: int = 0, world_size: int = 1,
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
                  seed: int = 0, devices=None, kind: str = "ladies", device_extract=False,
-                 pinned: Optional[bool] = None, device_count=None):
+                 pinned: Optional[bool] = None, device_count=None, skewed_sampling_nodes=None,
+                 scale_factor: float = 1.0):
         """device_count (LADIES, a graph without stored zeros): a torch device — the workers sum
-        U's column counts on it (gnn_colcount_*, the graph resident there) instead of on the host."""
+        U's column counts on it (gnn_colcount_*, the graph resident there) instead of on the host.
+        skewed_sampling_nodes (--locality_sampling, preprocess.py:414-423) are accepted at the
+        reference's scale_factor 1.0 (main.py:256), where they leave the draw unchanged
+        (sampler.py:119-121); scale_factor > 1 is the numpy branch (BatchLoader)."""
+        if float(scale_factor) > 1:
+            raise ValueError("NativeLoader draws at the reference's scale_factor 1.0 (main.py:256); "
+                             "scale_factor > 1 runs the numpy restatement: use BatchLoader")
+        self.skewed = skewed_sampling_nodes
         import scipy.sparse as sp
 
         from . import _lib

@@ -153,6 +153,17 @@ class DeviceBatch:
     sampled_nodes: list
     labels: torch.Tensor
     graph: Optional["DeviceGraph"] = None
+    # pinned host copy of the graph's extraction error flag, taken on the build stream right after
+    # this batch's GPU extractions (None when no layer was extracted on the GPU)
+    err_host: Optional[torch.Tensor] = None
+
+    def check_extraction(self) -> None:
+        """Raise if a GPU extraction up to and including this batch's saw a device count that
+        disagrees with the host's. The caller makes sure the build stream has passed the flag's
+        copy (StagedX0.wait synchronises on the staging event first)."""
+        if self.err_host is not None and int(self.err_host[0]):
+            raise RuntimeError(f"gnn_ladies_extract_f32: device counts disagree with the host's "
+                               f"(flag {int(self.err_host[0])}); the batch's operand is not used")
 
     def tensors(self) -> list:
         """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
@@ -200,6 +211,13 @@ class DeviceBatch:
             else:
                 adjs.append(op)
         self.adjs = adjs
+        if self.graph is not None and any(r is not None and r[2] is None for r in self.raw):
+            # the error flag as it stands after this batch's extractions, into pinned host memory on
+            # the same stream: read once the staging event has completed, before the step that
+            # consumes the operands is issued (StagedX0.wait)
+            if self.err_host is None:
+                self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self.err_host.copy_(self.graph.err, non_blocking=True)
         return adjs
 
 

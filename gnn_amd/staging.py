@@ -20,13 +20,14 @@ Here (DESIGN.md §Feature staging):
     kernel into X0. Either way the side stream runs ahead, overlapping the previous batch's
     aggregation kernels; the compute stream waits on an event only when it needs X0.
   * Peer rows (world_size > 1), two forms:
-    - ``PeerExchange`` (default): RCCL all-to-all — the request sizes and slot ids are
-      negotiated on the host over a gloo group (no GPU sync), each rank gathers the rows its
-      peers asked for from its own buffer, one all_to_all_single moves them over xGMI, and a
-      scatter kernel places them;
-    - ``PeerDirect`` (``--peer-rows direct``): every peer's buffer is mapped once (IPC) and the
-      staging stream's gather kernels read the batch's peer rows straight from the peers' HBM
-      over xGMI — no negotiation and no per-batch collective.
+    - ``PeerDirect`` (``--peer-rows direct``, the N > 1 default of bench.py; provisional until a
+      multi-GPU record's ``peer_rows_ab`` confirms it): every peer's buffer is mapped
+      once (IPC) and the staging stream's gather kernels read the batch's peer rows straight from
+      the peers' HBM over xGMI — no negotiation and no per-batch collective;
+    - ``PeerExchange`` (``--peer-rows alltoall``, and the fallback when any rank cannot map a
+      peer): RCCL all-to-all — the request sizes and slot ids are negotiated on the host over a
+      gloo group (no GPU sync), each rank gathers the rows its peers asked for from its own
+      buffer, one all_to_all_single moves them over xGMI, and a scatter kernel places them.
 """
 from __future__ import annotations
 
@@ -223,6 +224,9 @@ class Stager:
         return StagedX0(x0, ev, keep, self.store.F, batch)
 
 
+_EXTRACT_CHECK = os.environ.get("GNN_EXTRACT_CHECK", "step")
+
+
 class StagedX0:
     def __init__(self, x0, event, keep, F, batch=None):
         self._x0 = x0
@@ -238,6 +242,14 @@ class StagedX0:
         staged buffers were allocated on the staging stream and are read on this one: either
         each is marked with record_stream (default), or ``retire`` keeps them alive until the
         consuming step has run on the GPU (one event instead of ~40 record_stream calls)."""
+        b = self.batch
+        if b is not None and getattr(b, "err_host", None) is not None and _EXTRACT_CHECK == "step":
+            # GPU-extracted layers: their error flag is read before this step is issued, so a
+            # device count that disagrees with the host's raises before any kernel consumes the
+            # operand (a host wait on the staging event, which the staged work was issued a step
+            # ahead of; GNN_EXTRACT_CHECK=end defers the check to DeviceGraph.check at the end)
+            self.event.synchronize()
+            b.check_extraction()
         cur = torch.cuda.current_stream(self._x0.device)
         cur.wait_event(self.event)
         if retire is None:
@@ -396,11 +408,21 @@ class PeerExchange:
 
 
 def _ipc_close_all(mapped, device) -> None:
+    """Unmap the peers' buffers. The device is synchronised first, so no gather kernel still in
+    flight on any stream reads a mapping being closed (also when this runs as the finalizer of a
+    PeerDirect dropped without close())."""
     from . import _lib
 
+    if not mapped:
+        return
+    try:
+        torch.cuda.synchronize(device)
+    except RuntimeError:  # interpreter shutdown / a device already in error: unmap anyway
+        pass
     with _lib.on_device(device):
         for ptr, off in mapped:
             _lib.lib().gnn_ipc_close(ptr, off)
+    mapped.clear()
 
 
 class PeerDirect:
@@ -415,7 +437,12 @@ class PeerDirect:
     identically (``plan.peer_src``), so there is no per-batch negotiation and no collective:
     ranks never wait for each other while staging. The buffers never change after start-up,
     so no per-batch synchronisation with the peers is needed either. Same X0 as PeerExchange,
-    bit for bit (tests/test_dist_gpu.py)."""
+    bit for bit (tests/test_dist_gpu.py).
+
+    Callers must call the collective ``close()`` when staging is done (bench.py does so in a
+    ``finally``): it unmaps after a device sync and a barrier, so no rank frees its exported buffer
+    while a peer still reads it. The finalizer of an object dropped without close() only unmaps
+    this rank's mappings (after a device sync); it cannot wait for the peers."""
 
     needs_negotiation = False
 
@@ -436,6 +463,7 @@ class PeerDirect:
         buf = store.gpu_buffer
         self.ld = int(buf.stride(0))
         self.peers = [None] * self.world  # (mapped pointer, rows, ld) per peer rank
+        self.verified_rows = 0  # rows read through the mappings and checked against the feature table
         mapped = []
         self._closer = weakref.finalize(self, _ipc_close_all, mapped, dev)
         with stdout_to_stderr():
@@ -499,6 +527,7 @@ class PeerDirect:
             nodes = torch.from_numpy(np.asarray(buffer_nodes[j], np.int64)[slots])
             if not torch.equal(got[:, :F], feats[nodes]):
                 raise RuntimeError(f"rows read from rank {j}'s mapped buffer differ from the feature table")
+            self.verified_rows += len(slots)
 
     def prepare(self, plan: StagePlan):
         return None
@@ -509,6 +538,11 @@ class PeerDirect:
         torch.cuda.synchronize(self.device)
         self._closer()
         self.dist.barrier(group=self.group)
+
+    def close_local(self) -> None:
+        """Unmap this rank's mappings after a device sync, without waiting for the peers (the
+        error path: a peer may never reach close()'s barrier)."""
+        self._closer()
 
     def exchange(self, plan: StagePlan, x0: torch.Tensor, store: FeatureStore, meta=None):
         from . import _lib

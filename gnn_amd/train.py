@@ -90,6 +90,26 @@ class Trainer:
             for p, v in zip(self.params, _unflatten_dense_tensors(flat, self.params)):
                 p.copy_(v)
 
+    def param_digest(self) -> str:
+        """sha256 (first 16 hex digits) over every parameter's bytes, in parameter order."""
+        import hashlib
+
+        h = hashlib.sha256()
+        for p in self.params:
+            h.update(p.detach().contiguous().cpu().numpy().tobytes())
+        return h.hexdigest()[:16]
+
+    def check_ranks_agree(self) -> dict:
+        """Cross-rank consistency of the data-parallel step (main.py:146-170): after the summed
+        gradient and the same Adam update on every rank, all ranks must hold bit-identical
+        parameters. Collective (every rank of the group). Returns {"identical", "digests"}."""
+        d = self.param_digest()
+        if self.world <= 1:
+            return {"identical": True, "digests": [d]}
+        digests = [None] * self.world
+        torch.distributed.all_gather_object(digests, d, group=self.group)
+        return {"identical": all(x == digests[0] for x in digests), "digests": digests}
+
     def allreduce_grads(self) -> Optional[torch.Tensor]:
         """Σ over ranks of the (already clipped) gradients, in one flat buffer."""
         if self.world <= 1:

@@ -78,6 +78,15 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
 int gnn_spmm_config(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,
                     const void* X, const void* Y, int64_t unit_nnz, int32_t out[6]);
 
+/* The name of the main aggregation kernel gnn_spmm_csr_f32(_ex) would launch for this call, as
+ * rocprofv3 lists it: "spmm_unit_kernel<VW, G, NJ, U, RES>" (nnz work units + the combine of
+ * cut rows) or, for small operands (up to 64 k nonzeros, unit_nnz == 0: the layer-2 calls),
+ * "spmm_row_kernel<VW, NJ, U, WPR, RES>" (a workgroup of WPR waves per (row, column slice), no
+ * combine launch). residual != 0 names the row-mapped residual variant. */
+int gnn_spmm_kernel_name(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy,
+                         const void* X, const void* Y, int64_t unit_nnz, int residual, char* out,
+                         size_t out_bytes);
+
 /* Optional timing hook: when set, the NEXT gnn_spmm_csr_f32 call on this thread records
  * `start` immediately before and `stop` immediately after its main aggregation kernel on
  * the call's stream, then clears the hook. Events are hipEvent_t passed as void*. */

@@ -248,3 +248,31 @@ def test_gpu_extraction_hub_rows(dev):
             for k in ("rowptr", "col", "val"):
                 assert torch.equal(getattr(a.transpose(), k), getattr(b.transpose(), k)), (li, "t", k)
     dd.graph.check()
+
+
+@pytest.mark.gpu
+def test_count_mismatch_raises_before_the_step(dev):
+    """A GPU-extracted layer whose device count disagrees with the host's raises when the staged
+    batch is handed to its step (StagedX0.wait, before any kernel of the step is issued), not at
+    the end of the run: the flag is copied to pinned memory on the staging stream right after the
+    batch's extractions."""
+    from gnn_amd import staging
+
+    hb, hd = _pair("symmetric", [1, 1, 1], 300, 64, 7)
+    dd = hd.to_device(dev, with_coo=False)
+    ev = torch.cuda.Event()
+    ev.record()
+    x0 = torch.zeros(4, 8, device=dev)
+    assert dd.err_host is not None
+    staging.StagedX0(x0, ev, (), 8, dd).wait()  # a consistent batch passes
+    li = next(i for i, L in enumerate(hd.layers) if L is not None and L.on_device)
+    hd.layers[li].dev_nnz += 1  # the host's count now disagrees with the device's
+    bad = hd.to_device(dev, with_coo=False)
+    ev = torch.cuda.Event()
+    ev.record()
+    try:
+        with pytest.raises(RuntimeError, match="disagree"):
+            staging.StagedX0(x0, ev, (), 8, bad).wait()
+    finally:
+        torch.cuda.synchronize()
+        bad.graph.err.zero_()

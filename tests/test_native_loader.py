@@ -168,3 +168,55 @@ def test_blob_dropped_right_after_upload(dev):
             del next_lb
     finally:
         b.close()
+
+
+def test_locality_sampling_leaves_the_draw_unchanged_at_scale_1():
+    """--locality_sampling (main.py:284-287): the skewed node sets (preprocess.py:414-423) reach
+    every sampler call; at the reference's scale_factor 1.0 (main.py:256) they do not change the
+    draw (sampler.py:119-121) — the native producer with the flag yields the same batches, bit for
+    bit, as without it. With scale_factor > 1 the numpy branch boosts the skewed nodes (the draw
+    then differs), and the native producer refuses it."""
+    import scipy.sparse as sp
+
+    lap, labels, feats, train, pl = _setup(world=2)
+    A = (lap != 0).astype(np.float32).tocsr()
+    skew = placement.get_skewed_sampled_nodes(A + sp.eye(A.shape[0], dtype=np.float32, format="csr"),
+                                              pl.gpu_buffer_group, [1, 1, 1])
+    assert len(skew) == 3 and all(len(s) > 0 for s in skew)
+    dev_of, idx_on = pl.device_id_of_nodes_group[1], pl.idx_of_nodes_on_device_group[1]
+    kw = dict(rank=1, world_size=2, workers=2, seed=5, kind="ladies", device_extract=True)
+    plain = loader.NativeLoader(lap, labels, train, 300, 64, [1, 1, 1], dev_of, idx_on, **kw)
+    flag = loader.NativeLoader(lap, labels, train, 300, 64, [1, 1, 1], dev_of, idx_on, **kw,
+                               skewed_sampling_nodes=skew, scale_factor=1.0)
+    py = loader.BatchLoader(lap, labels, train, 300, 64, [1, 1, 1], dev_of, idx_on, **kw,
+                            skewed_sampling_nodes=skew, scale_factor=1.0)
+    try:
+        n = 0
+        for a, b, c in zip(plain.epoch(1), flag.epoch(1), py.epoch(1)):
+            for other in (b.host, c.host):
+                _eq(a.host.input_nodes, other.input_nodes, "input nodes")
+                for La, Lb in zip(a.host.layers, other.layers):
+                    assert La.nnz == Lb.nnz
+                    for k in ("fullrowptr", "rowptr", "colidx", "normfact", "rows", "cols"):
+                        va, vb = getattr(La, k), getattr(Lb, k)
+                        assert (va is None) == (vb is None)
+                        if va is not None:
+                            _eq(va, vb, k)
+            n += 1
+            if n == 4:
+                break
+    finally:
+        plain.close()
+        flag.close()
+        py.close()
+    with pytest.raises(ValueError, match="scale_factor"):
+        loader.NativeLoader(lap, labels, train, 300, 64, [1, 1, 1], dev_of, idx_on, **kw,
+                            skewed_sampling_nodes=skew, scale_factor=2.0)
+    # scale_factor > 1 (numpy branch): the boosted nodes change the draw
+    batch = sampler.rank_batches(train, 64, 1, 2, 1)[0]
+    args = (3, batch, np.array([300] * 5), lap.shape[0], lap, labels, [1, 1, 1], dev_of, idx_on)
+    h1 = sampler.ladies_sample_host(*args, skew, 1.0, [0, 1], native=False)
+    h4 = sampler.ladies_sample_host(*args, skew, 4.0, [0, 1], native=False)
+    assert not np.array_equal(h1.input_nodes, h4.input_nodes)
+    hn = sampler.ladies_sample_host(*args, skew, 1.0, [0, 1])
+    _eq(h1.input_nodes, hn.input_nodes, "numpy == native at scale 1")

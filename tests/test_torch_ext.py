@@ -176,3 +176,20 @@ def test_module_in_the_reference_autograd_pattern(dev):
     np.testing.assert_allclose(Y.detach().cpu().numpy(), O.spmm_f32(rowptr, ocol, oval, X), rtol=RTOL, atol=ATOL)
     trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K)
     np.testing.assert_allclose(Xd.grad.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
+
+
+@pytest.mark.gpu
+def test_module_create_coo_tensor_sums_duplicate_columns(dev):
+    from oracle.fixtures import coalesced_reference, duplicate_columns_case
+
+    mod = torch_ops.load()
+    M, K, full, rowptr, col, nf = duplicate_columns_case()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    A = mod.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int32)), t(nf), M, K)
+    ref = coalesced_reference(M, K, full, rowptr, col, nf)
+    assert A.is_coalesced() and A._nnz() == 10
+    assert torch.equal(A._indices().cpu(), ref._indices())
+    np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
+    X = torch.randn(K, 40, device=dev)
+    np.testing.assert_allclose(mod.spmm_load_balance(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(),
+                               rtol=1e-5, atol=1e-5)
