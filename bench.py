@@ -380,14 +380,23 @@ def run_cpu(args, spec, A, lap, labels, feats, num_classes, train):
 def roofline_from(recs, step_batches, args, traffic, steps):
     """Per call site and for the dominant aggregation kernel: algorithmic, compulsory and
     (PMC) L2-egress byte rates over the HIP-event launch durations of the distinct-batch run.
-    Call sites per step, in call order: 3 forwards, then the backwards of layers 2 and 1."""
+    Call sites per step, in call order: 3 forwards, then the backwards of layers 2 and 1 (the
+    executor folds the layer-2 backward into the layer-1 tail when its rows are short: no record)."""
     names = ["fwd_L0", "fwd_L1", "fwd_L2", "bwd_L2", "bwd_L1"]
     site, kname = {}, {}
     uniq_cache = {}
+    step_i, prev = 0, None
     for i, (tag, ms, nbytes, kn, dims) in enumerate(recs):
-        key = names[i % len(names)]
-        assert key.startswith(tag), (key, tag)
-        hb, db = step_batches[(i // len(names)) % len(step_batches)]
+        if "_L" in tag:  # the executor names its call sites (a folded call site has no record)
+            key = tag
+            if prev is not None and names.index(key) <= names.index(prev):
+                step_i += 1
+            prev = key
+        else:  # the autograd path: 5 calls per step in call order
+            key = names[i % len(names)]
+            assert key.startswith(tag), (key, tag)
+            step_i = i // len(names)
+        hb, db = step_batches[step_i % len(step_batches)]
         li = int(key[-1])
         L = hb.layers[li]
         ck = (id(hb), key)

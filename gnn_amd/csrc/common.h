@@ -19,6 +19,12 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // out[0..n] = exclusive prefix of in[0..n) (out[n] = total), one workgroup (spmm.hip).
 int launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st);
 
+// Whether gnn_spmm_csr_f32(_ex) runs this call shape as spmm_row_kernel with one wave per row
+// (every output a C fmaf chain over the row in CSR order): the executor then may fold the call
+// into its consumer (gnn_sage_norm_bwd_agg_f32) with bit-identical values.
+bool spmm_row_chain(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+                    const void* Y);
+
 // gnn_gemm_f32_split3 with the split-k choice made for a batch of split_nbatch products
 // (gemm.hip): one product of a batch launched on its own, bit-identical to the batched result.
 int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, int split_nbatch,

@@ -81,6 +81,76 @@ __device__ __forceinline__ f4 load_h(const float* hB, int64_t ldb, const float* 
   return h;
 }
 
+// The output gradient of a row: a dense row of gY, or (AGG) computed on the fly as the
+// aggregation Aᵀ·G of the layer above plus its row-mapped residual — the layer-2 backward
+// aggregation fused into the layer-1 tail (gnn_sage_norm_bwd_agg_f32): Aᵀ's rows are short
+// (1.7 nonzeros on average for the Reddit batch) and G is L2-resident, so the tail reads those
+// few G rows instead of a 35 MB gradient that a separate launch would write and this kernel
+// read back. Per element the same operations in the same order as spmm_row_kernel with one wave
+// per row (a C fmaf chain over the row in CSR order from 0, then + the residual): bit-identical.
+struct GradSrc {
+  const float* gY;
+  int64_t ldg;
+  const int* rp;  // Aᵀ (rows = this layer's rows), CSR
+  const int* col;
+  const float* val;
+  const float* G;  // the dense operand Aᵀ multiplies (rows of the layer above)
+  int64_t ldG;
+  const float* R;  // residual rows R[rmap[r]] (rmap NULL: none)
+  int64_t ldr;
+  const int* rmap;
+};
+
+__device__ __forceinline__ f4 fma4(float v, f4 x, f4 a) {
+  return f4{__builtin_fmaf(v, x.x, a.x), __builtin_fmaf(v, x.y, a.y), __builtin_fmaf(v, x.z, a.z),
+            __builtin_fmaf(v, x.w, a.w)};
+}
+
+// g[k] for columns cbase + (lane + 64 k) * 4 < cend of row r.
+template <bool AGG, int NV>
+__device__ __forceinline__ void grad_row(const GradSrc& s, int r, int lane, int cbase, int cend, f4 (&g)[NV]) {
+  if constexpr (!AGG) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = cbase + (lane + 64 * k) * 4;
+      g[k] = c < cend ? *reinterpret_cast<const f4*>(s.gY + (int64_t)r * s.ldg + c) : f4(0.0f);
+    }
+  } else {
+    const int q = s.rmap ? s.rmap[r] : -1;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) g[k] = f4(0.0f);
+    const int rb = s.rp[r], re = s.rp[r + 1];
+    // two nonzeros per round: both G rows in flight before the FMAs (added in CSR order)
+    for (int e = rb; e < re; e += 2) {
+      const bool two = e + 1 < re;  // wave-uniform
+      const float* x0 = s.G + (int64_t)s.col[e] * s.ldG;  // wave-uniform: scalar loads of (col, val)
+      const float v0 = s.val[e];
+      const float* x1 = two ? s.G + (int64_t)s.col[e + 1] * s.ldG : x0;
+      const float v1 = two ? s.val[e + 1] : 0.0f;
+      f4 xs0[NV], xs1[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = cbase + (lane + 64 * k) * 4;
+        xs0[k] = c < cend ? *reinterpret_cast<const f4*>(x0 + c) : f4(0.0f);
+        xs1[k] = (two && c < cend) ? *reinterpret_cast<const f4*>(x1 + c) : f4(0.0f);
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) g[k] = fma4(v0, xs0[k], g[k]);
+      if (two) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) g[k] = fma4(v1, xs1[k], g[k]);
+      }
+    }
+    if (q >= 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = cbase + (lane + 64 * k) * 4;
+        if (c < cend) g[k] += *reinterpret_cast<const f4*>(s.R + (int64_t)q * s.ldr + c);
+      }
+    }
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restrict__ hB, int64_t ldb,
                                                             const float* __restrict__ bB, int D1,
@@ -142,9 +212,9 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
   }
 }
 
-template <int NV>
+template <int NV, bool AGG>
 __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
-    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb,
+    GradSrc src, const float* __restrict__ hB, int64_t ldb,
     const float* __restrict__ bB, int D1, const float* __restrict__ hW, int64_t ldw, const float* __restrict__ bW,
     int D, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd, int M,
     float p, float inv_keep, uint64_t seed, int training, float* __restrict__ dhB, float* __restrict__ dhW,
@@ -163,17 +233,23 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
     const float m = mean[r];
     const float rs = rstd[r];
     f4 h[NV], xh[NV], gx[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {  // pre-activations first (overlapping the gradient's chain)
+      const int c = (lane + 64 * k) * 4;
+      h[k] = c < D ? load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c) : f4(0.0f);
+    }
+    grad_row<AGG, NV>(src, r, lane, 0, D, gx);  // gx holds the output gradient until it is scaled
     float a = 0.0f, b = 0.0f;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int c = (lane + 64 * k) * 4;
       if (c < D) {
-        const f4 hk = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
+        const f4 hk = h[k];
         const f4 o = f4{elu1(hk.x), elu1(hk.y), elu1(hk.z), elu1(hk.w)};
         h[k] = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
                   elu1_grad_from_out(o.w)};  // h[k] now holds the ELU derivative
         xh[k] = (o - m) * rs;
-        f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
+        f4 g = gx[k];
         if (training) {
           const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
           g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
@@ -230,9 +306,9 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
 // barrier per row pair, double-buffered by iteration parity.
 constexpr int BWD2_MAX_GRID = 1024;
 
-template <int NVH>
+template <int NVH, bool AGG>
 __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
-    const float* __restrict__ gY, int64_t ldg, const float* __restrict__ hB, int64_t ldb,
+    GradSrc src, const float* __restrict__ hB, int64_t ldb,
     const float* __restrict__ bB, int D1, const float* __restrict__ hW, int64_t ldw, const float* __restrict__ bW,
     int D, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd, int M,
     float p, float inv_keep, uint64_t seed, int training, float* __restrict__ dhB, float* __restrict__ dhW,
@@ -259,20 +335,29 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
     f4 eg[NVH], xh[NVH], gx[NVH];
     float a = 0.0f, b = 0.0f;
     float m = 0.0f, rs = 0.0f;
+    f4 hv[NVH];
     if (live) {
       m = mean[r];
       rs = rstd[r];
+      // the row's pre-activations first: their loads overlap the gradient's dependent chain
+      // (Aᵀ row pointer -> (col, val) -> G rows) when the gradient is aggregated here
+#pragma unroll
+      for (int k = 0; k < NVH; ++k) {
+        const int c = cbase + (lane + 64 * k) * 4;
+        hv[k] = c < cend ? load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c) : f4(0.0f);
+      }
+      grad_row<AGG, NVH>(src, r, lane, cbase, cend, gx);  // the output gradient, scaled below
     }
 #pragma unroll
     for (int k = 0; k < NVH; ++k) {
       const int c = cbase + (lane + 64 * k) * 4;
       if (live && c < cend) {
-        const f4 hk = load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c);
+        const f4 hk = hv[k];
         const f4 o = f4{elu1(hk.x), elu1(hk.y), elu1(hk.z), elu1(hk.w)};
         eg[k] = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
                    elu1_grad_from_out(o.w)};
         xh[k] = (o - m) * rs;
-        f4 g = *reinterpret_cast<const f4*>(gY + (int64_t)r * ldg + c);
+        f4 g = gx[k];
         if (training) {
           const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
           g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
@@ -382,7 +467,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float
 
 using FwdFn = void (*)(const float*, int64_t, const float*, int, const float*, int64_t, const float*, int,
                        const float*, const float*, int, float, float, uint64_t, int, float*, int64_t, float*, float*);
-using BwdFn = void (*)(const float*, int64_t, const float*, int64_t, const float*, int, const float*, int64_t,
+using BwdFn = void (*)(GradSrc, const float*, int64_t, const float*, int, const float*, int64_t,
                        const float*, int, const float*, const float*, const float*, int, float, float, uint64_t, int,
                        float*, float*, float*);
 
@@ -400,12 +485,13 @@ FwdFn fwd_fn(int nv) {
   }
 }
 
+template <bool AGG>
 BwdFn bwd2_fn(int nvh) {
   switch (nvh) {
-    case 1: return &sage_norm_bwd2_kernel<1>;
-    case 2: return &sage_norm_bwd2_kernel<2>;
-    case 3: return &sage_norm_bwd2_kernel<3>;
-    case 4: return &sage_norm_bwd2_kernel<4>;
+    case 1: return &sage_norm_bwd2_kernel<1, AGG>;
+    case 2: return &sage_norm_bwd2_kernel<2, AGG>;
+    case 3: return &sage_norm_bwd2_kernel<3, AGG>;
+    case 4: return &sage_norm_bwd2_kernel<4, AGG>;
     default: return nullptr;
   }
 }
@@ -419,16 +505,17 @@ int64_t bwd_grid(int64_t M, int64_t D) {
   return std::max<int64_t>(1, ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap);
 }
 
+template <bool AGG>
 BwdFn bwd_fn(int nv) {
   switch (nv) {
-    case 1: return &sage_norm_bwd_kernel<1>;
-    case 2: return &sage_norm_bwd_kernel<2>;
-    case 3: return &sage_norm_bwd_kernel<3>;
-    case 4: return &sage_norm_bwd_kernel<4>;
-    case 5: return &sage_norm_bwd_kernel<5>;
-    case 6: return &sage_norm_bwd_kernel<6>;
-    case 7: return &sage_norm_bwd_kernel<7>;
-    case 8: return &sage_norm_bwd_kernel<8>;
+    case 1: return &sage_norm_bwd_kernel<1, AGG>;
+    case 2: return &sage_norm_bwd_kernel<2, AGG>;
+    case 3: return &sage_norm_bwd_kernel<3, AGG>;
+    case 4: return &sage_norm_bwd_kernel<4, AGG>;
+    case 5: return &sage_norm_bwd_kernel<5, AGG>;
+    case 6: return &sage_norm_bwd_kernel<6, AGG>;
+    case 7: return &sage_norm_bwd_kernel<7, AGG>;
+    case 8: return &sage_norm_bwd_kernel<8, AGG>;
     default: return nullptr;
   }
 }
@@ -476,11 +563,17 @@ size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
   return gnn::align_up((size_t)G * NRED * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
 }
 
-int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
-                          int64_t ldw, int64_t D2, const float* biasB, const float* biasW, const float* scale,
-                          const float* mean, const float* rstd, int64_t M, float p_drop, uint64_t seed, int training,
-                          float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int sage_norm_bwd(const GradSrc& src, bool agg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
+                  int64_t ldw, int64_t D2, const float* biasB, const float* biasW, const float* scale,
+                  const float* mean, const float* rstd, int64_t M, float p_drop, uint64_t seed, int training,
+                  float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
+                  void* workspace, size_t workspace_bytes, void* stream) {
+  const float* gY = agg ? src.G : src.gY;
+  const int64_t ldg = agg ? 4 : src.ldg;
   int rc = check_shapes("gnn_sage_norm_bwd_f32", D1, D2, M, hB, ldb, hW, ldw, biasB, biasW);
   if (rc) return rc;
   GNN_REQUIRE(scale && dscale && doffset, "gnn_sage_norm_bwd_f32: NULL pointer");
@@ -504,19 +597,63 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
   const float inv_keep = 1.0f / (1.0f - p_drop);
   float* partial = (float*)workspace;
   if (use_bwd2(D)) {
-    hipLaunchKernelGGL(bwd2_fn((int)ceil_div(D / 2, 256)), dim3((unsigned)G), dim3(256), (size_t)2 * D * sizeof(float),
-                       st, gY, ldg, hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M,
-                       p_drop, inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
+    hipLaunchKernelGGL(agg ? bwd2_fn<true>((int)ceil_div(D / 2, 256)) : bwd2_fn<false>((int)ceil_div(D / 2, 256)),
+                       dim3((unsigned)G), dim3(256), (size_t)2 * D * sizeof(float), st, src, hB ? hB : hW, ldb, biasB,
+                       (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop, inv_keep, seed, training,
+                       dhB ? dhB : dhW, dhW, partial);
   } else {
-    hipLaunchKernelGGL(bwd_fn((int)ceil_div(D, 256)), dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st,
-                       gY, ldg, hB ? hB : hW, ldb, biasB, (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop,
-                       inv_keep, seed, training, dhB ? dhB : dhW, dhW, partial);
+    hipLaunchKernelGGL(agg ? bwd_fn<true>((int)ceil_div(D, 256)) : bwd_fn<false>((int)ceil_div(D, 256)),
+                       dim3((unsigned)G), dim3(256), (size_t)4 * D * sizeof(float), st, src, hB ? hB : hW, ldb, biasB,
+                       (int)D1, hW, ldw, biasW, D, scale, mean, rstd, (int)M, p_drop, inv_keep, seed, training,
+                       dhB ? dhB : dhW, dhW, partial);
   }
   GNN_LAUNCHED("sage_norm_bwd_kernel");
   sage_norm_bwd_finalize_kernel<<<dim3((unsigned)ceil_div(NRED * D, FIN_COLS)), dim3(256), 0, st>>>(
       partial, (int)G, D, (int)D1, dscale, doffset, dbiasB, dbiasW);
   GNN_LAUNCHED("sage_norm_bwd_finalize_kernel");
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t ldb, int64_t D1, const float* hW,
+                          int64_t ldw, int64_t D2, const float* biasB, const float* biasW, const float* scale,
+                          const float* mean, const float* rstd, int64_t M, float p_drop, uint64_t seed, int training,
+                          float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  GradSrc src{};
+  src.gY = gY;
+  src.ldg = ldg;
+  return sage_norm_bwd(src, false, hB, ldb, D1, hW, ldw, D2, biasB, biasW, scale, mean, rstd, M, p_drop, seed,
+                       training, dhB, dhW, dscale, doffset, dbiasB, dbiasW, workspace, workspace_bytes, stream);
+}
+
+int gnn_sage_norm_bwd_agg_f32(const int32_t* t_rowptr, const int32_t* t_col, const float* t_val, const float* G,
+                              int64_t ldG, const float* R, int64_t ldr, const int32_t* rmap, const float* hB,
+                              int64_t ldb, int64_t D1, const float* hW, int64_t ldw, int64_t D2, const float* biasB,
+                              const float* biasW, const float* scale, const float* mean, const float* rstd, int64_t M,
+                              float p_drop, uint64_t seed, int training, float* dhB, float* dhW, float* dscale,
+                              float* doffset, float* dbiasB, float* dbiasW, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  const int64_t D = D1 + D2;
+  GNN_REQUIRE(M == 0 || (t_rowptr && G), "gnn_sage_norm_bwd_agg_f32: NULL t_rowptr / G");
+  GNN_REQUIRE(ldG % 4 == 0 && (uintptr_t)G % 16 == 0 && ldG >= D, "gnn_sage_norm_bwd_agg_f32: G must be 16-byte "
+              "aligned rows of at least D floats");
+  GNN_REQUIRE(rmap == nullptr || (R && ldr % 4 == 0 && (uintptr_t)R % 16 == 0 && ldr >= D),
+              "gnn_sage_norm_bwd_agg_f32: R must be 16-byte aligned rows of at least D floats");
+  GradSrc src{};
+  src.rp = t_rowptr;
+  src.col = t_col;
+  src.val = t_val;
+  src.G = G;
+  src.ldG = ldG;
+  src.R = R;
+  src.ldr = ldr;
+  src.rmap = rmap;
+  return sage_norm_bwd(src, true, hB, ldb, D1, hW, ldw, D2, biasB, biasW, scale, mean, rstd, M, p_drop, seed,
+                       training, dhB, dhW, dscale, doffset, dbiasB, dbiasW, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -1214,6 +1214,13 @@ void pick_row_kernel(SpmmCfg& c, int64_t M, int64_t nnz, int64_t F, int64_t unit
   if (c.vw == 4 && M >= 4096) nj = chunks >= 4 ? 4 : (chunks >= 2 ? 2 : 1);
   const int64_t slices = ceil_div(chunks, (int64_t)nj);
   const double avg = (double)nnz / (double)M;
+  // Measured on the layer-2 calls (profiles/round4/layer2/): short rows (the backward's Aᵀ, 1.7
+  // nonzeros per row) 12.7-13.7 us with 1-2 waves per row against 25 us for units + combine;
+  // long-tailed rows (the forward's A, 29 per row, up to 484) 20.4 us at best (8 waves per row)
+  // against 19.5 for units + combine — so by default only short-row operands take this kernel,
+  // with one wave per row (each output a C fmaf chain: the executor folds such a call into the
+  // tail that consumes it, gnn_sage_norm_bwd_agg_f32, bit for bit).
+  if (mode != 1 && avg >= 12.0) return;
   int wpr = avg >= 48.0 ? 8 : (avg >= 12.0 ? 4 : 1);
   if (const char* e = getenv("GNN_SPMM_ROWK_WPR")) {  // experiments
     const int v = atoi(e);
@@ -1483,6 +1490,12 @@ int run_segsort(const int* ptr, int64_t nseg, int* key, float* val, void* ws, hi
 }
 
 }  // namespace
+
+bool gnn::spmm_row_chain(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
+                         const void* Y) {
+  const SpmmCfg c = make_cfg(M, K, nnz, F, ldx, ldy, X, Y, 0);
+  return c.wpr == 1 && c.vw == 4;
+}
 
 int gnn::launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st) {
   scan_exclusive_kernel<<<dim3(1), dim3(1024), 0, st>>>(in, n, out, nullptr);

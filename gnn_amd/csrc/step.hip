@@ -183,6 +183,13 @@ size_t gemm_ws(int64_t M, int64_t N, int64_t K, int nb) {
 // GNN_STEP_OVERLAP=1 turns the aux stream on. Off by default: measured on the Reddit config-2
 // step it changed nothing (550 mini-batches/s either way; the layer-0/1 aggregations slowed from
 // 239 to 261 us while the GEMMs ran beside them — the CUs are already saturated).
+// GNN_STEP_FUSE_AGG=0: launch the top layer's backward aggregation on its own instead of folding
+// it into the layer-1 tail backward (A/B; the values are bit-identical either way)
+bool fuse_agg_enabled() {
+  const char* e = getenv("GNN_STEP_FUSE_AGG");  // read per step (tests toggle it in-process)
+  return !(e && atoi(e) == 0);
+}
+
 bool overlap_enabled() {
   static const bool on = [] {
     const char* e = getenv("GNN_STEP_OVERLAP");
@@ -225,6 +232,11 @@ struct LayerBufs {
   float *dY, *dhB, *dhW, *dxs, *dfeat;
   void *ws_fwd, *ws_bwd, *ws_norm, *ws_gemm_f, *ws_gemm_f2, *ws_gemm_dx, *ws_gemm_dw;
   size_t b_fwd, b_bwd, b_norm, b_gemm_f, b_gemm_dx, b_gemm_dw;
+  // dY given as the aggregation of the layer above (its backward SpMM folded into this layer's
+  // tail backward, gnn_sage_norm_bwd_agg_f32) instead of a dense buffer
+  bool dy_agg;
+  const int32_t *agg_rp, *agg_col, *agg_rmap;
+  const float *agg_val, *agg_G, *agg_R;
 };
 
 struct Plan {
@@ -244,6 +256,7 @@ int plan(const int64_t* d, Arena& ar, Plan& pl) {
   const int n = pl.sage ? 2 : 1;
   for (int l = 0; l < pl.nl; ++l) {
     LayerBufs& b = pl.lb[l];
+    b.dy_agg = false;
     b.M = L(d, l, GNN_SL_M);
     b.K = L(d, l, GNN_SL_K);
     b.nnz = L(d, l, GNN_SL_NNZ);
@@ -477,12 +490,23 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     const int64_t N = b.N;
     const float* WB = P<const float>(d, l, GNN_SL_WB);
     const float* WW = P<const float>(d, l, GNN_SL_WW);
-    GNN_TRY(gnn_sage_norm_bwd_f32(b.dY, b.D, pl.sage ? b.hB : nullptr, pl.sage ? N : 4, pl.sage ? N : 0, b.hW, N, N,
-                                  pl.sage ? P<const float>(d, l, GNN_SL_BB) : nullptr, P<const float>(d, l, GNN_SL_BW),
-                                  P<const float>(d, l, GNN_SL_SCALE), b.mean, b.rstd, b.M, p,
-                                  (uint64_t)L(d, l, GNN_SL_SEED), training, b.dhB, b.dhW, P<float>(d, l, GNN_SL_GSCALE),
-                                  P<float>(d, l, GNN_SL_GOFFSET), pl.sage ? P<float>(d, l, GNN_SL_GBB) : nullptr,
-                                  P<float>(d, l, GNN_SL_GBW), b.ws_norm, b.b_norm, st));
+    if (b.dy_agg)  // the layer above's backward aggregation, computed as this tail reads its rows
+      GNN_TRY(gnn_sage_norm_bwd_agg_f32(b.agg_rp, b.agg_col, b.agg_val, b.agg_G, b.D, b.agg_R, b.D, b.agg_rmap,
+                                        pl.sage ? b.hB : nullptr, pl.sage ? N : 4, pl.sage ? N : 0, b.hW, N, N,
+                                        pl.sage ? P<const float>(d, l, GNN_SL_BB) : nullptr,
+                                        P<const float>(d, l, GNN_SL_BW), P<const float>(d, l, GNN_SL_SCALE), b.mean,
+                                        b.rstd, b.M, p, (uint64_t)L(d, l, GNN_SL_SEED), training, b.dhB, b.dhW,
+                                        P<float>(d, l, GNN_SL_GSCALE), P<float>(d, l, GNN_SL_GOFFSET),
+                                        pl.sage ? P<float>(d, l, GNN_SL_GBB) : nullptr, P<float>(d, l, GNN_SL_GBW),
+                                        b.ws_norm, b.b_norm, st));
+    else
+      GNN_TRY(gnn_sage_norm_bwd_f32(b.dY, b.D, pl.sage ? b.hB : nullptr, pl.sage ? N : 4, pl.sage ? N : 0, b.hW, N, N,
+                                    pl.sage ? P<const float>(d, l, GNN_SL_BB) : nullptr, P<const float>(d, l, GNN_SL_BW),
+                                    P<const float>(d, l, GNN_SL_SCALE), b.mean, b.rstd, b.M, p,
+                                    (uint64_t)L(d, l, GNN_SL_SEED), training, b.dhB, b.dhW,
+                                    P<float>(d, l, GNN_SL_GSCALE), P<float>(d, l, GNN_SL_GOFFSET),
+                                    pl.sage ? P<float>(d, l, GNN_SL_GBB) : nullptr, P<float>(d, l, GNN_SL_GBW),
+                                    b.ws_norm, b.b_norm, st));
     const bool ok = gemm_ok(b.feat, b.ldo) && gemm_ok(WW, b.F) && (!pl.sage || gemm_ok(WB, b.F));
     const float* G[2] = {pl.sage ? b.dhB : b.dhW, b.dhW};
     const int o = pl.sage ? 0 : 1;
@@ -526,7 +550,20 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     if (l >= 1) {  // dY_{l-1} = A_lᵀ·dfeat (+ dxs through rmap: the x[sampled] gradient)
       LayerBufs& prev = pl.lb[l - 1];
       GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_TROWPTR) != nullptr, "gnn_train_step: layer %d has no transpose", l);
-      if (pl.sage) {
+      if (pl.sage) GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_RMAP) != nullptr, "gnn_train_step: layer %d has no row map", l);
+      // short-row transposes (the top layer's: 1.7 nonzeros per row on the Reddit batch) that a
+      // standalone call would run as one fmaf chain per row: folded into layer l-1's tail
+      // backward, which computes each dY row as it reads it (no dY write / read back, no launch)
+      if (fuse_agg_enabled() && prev.D == b.F &&
+          gnn::spmm_row_chain(b.K, b.M, b.nnz, b.F, b.F, b.F, b.dfeat, prev.dY)) {
+        prev.dy_agg = true;
+        prev.agg_rp = P<const int32_t>(d, l, GNN_SL_TROWPTR);
+        prev.agg_col = P<const int32_t>(d, l, GNN_SL_TCOL);
+        prev.agg_val = P<const float>(d, l, GNN_SL_TVAL);
+        prev.agg_G = b.dfeat;
+        prev.agg_R = pl.sage ? b.dxs : nullptr;
+        prev.agg_rmap = pl.sage ? P<const int32_t>(d, l, GNN_SL_RMAP) : nullptr;
+      } else if (pl.sage) {
         GNN_REQUIRE(P<const int32_t>(d, l, GNN_SL_RMAP) != nullptr, "gnn_train_step: layer %d has no row map", l);
         arm(1, l, b.K, b.M, b.nnz, b.F, b.F, b.F, b.F, b.dfeat, prev.dY, b.M);
         GNN_TRY(gnn_spmm_csr_f32_ex(P<const int32_t>(d, l, GNN_SL_TROWPTR), P<const int32_t>(d, l, GNN_SL_TCOL),

@@ -209,5 +209,5 @@ class NativeStep:
             if r[14] != 1:
                 continue
             kind, l, M, K, nnz, F, Fk, ldx, ldy, xp, yp, res = (int(v) for v in r[2:14])
-            cso.record_timing("fwd" if kind == 0 else "bwd", e0, e1, M, K, nnz, F, Fk, ldx, ldy, xp, yp, 0, res,
-                              kind == 1 and res > 0)
+            cso.record_timing(("fwd" if kind == 0 else "bwd") + f"_L{l}", e0, e1, M, K, nnz, F, Fk, ldx, ldy, xp, yp,
+                              0, res, kind == 1 and res > 0)

@@ -41,6 +41,23 @@ int gnn_sage_norm_bwd_f32(const float* gY, int64_t ldg, const float* hB, int64_t
                           float* dhB, float* dhW, float* dscale, float* doffset, float* dbiasB, float* dbiasW,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* gnn_sage_norm_bwd_f32 whose output gradient is not a dense gY but the aggregation of the layer
+ * above, computed per row as the tail reads it:
+ *   gY[r] = Σ_e t_val[e] · G[t_col[e]]  (e over Aᵀ's row r, a C fmaf chain from 0 in CSR order)
+ *           + R[rmap[r]]               (when rmap[r] >= 0; rmap NULL: no residual)
+ * — the same values gnn_spmm_csr_f32_ex produces for this operand with its row kernel (one wave
+ * per row), bit for bit. Replaces the backward aggregation of the top layer (custom_sparse_ops.py:
+ * 33-37, A.t().coalesce() @ G, and GraphSAGE's x[sampled] gradient scatter) when Aᵀ's rows are
+ * short: the 35 MB gradient is never written nor read back. G and R: 16-byte aligned rows of at
+ * least D floats. */
+int gnn_sage_norm_bwd_agg_f32(const int32_t* t_rowptr, const int32_t* t_col, const float* t_val, const float* G,
+                              int64_t ldG, const float* R, int64_t ldr, const int32_t* rmap, const float* hB,
+                              int64_t ldb, int64_t D1, const float* hW, int64_t ldw, int64_t D2, const float* biasB,
+                              const float* biasW, const float* scale, const float* mean, const float* rstd, int64_t M,
+                              float p_drop, uint64_t seed, int training, float* dhB, float* dhW, float* dscale,
+                              float* doffset, float* dbiasB, float* dbiasW, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
 /* ---------------------------------------------------------------------------------
  * fp32 GEMMs of the layers on gfx950 MFMA (gemm.hip): C[b] = A[b] · B[b] for b < nbatch
  * (1..4 problems of one shape in one launch; A, B, C are HOST arrays of device pointers).

@@ -1,0 +1,21 @@
+# Round-4 GPU pass d: the whole GPU suite (row kernel, folded layer-2 backward, config-3 staging
+# at world 4), the folded-vs-launched A/B/A/B under the bench, and the bench under rocprofv3.
+set -o pipefail
+TAG=${1:-r4d}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+REPO=$(pwd)
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/gputest_$TAG.log 2>&1 || { echo "tests failed"; exit 1; }
+for v in 1 0 1 0; do
+  GNN_STEP_FUSE_AGG=$v timeout -k 10 300 python -u bench.py --steps 300 --no-cpu-baseline --no-traffic \
+      > gpurun_out/bench_fuse${v}_$TAG.$RANDOM.json 2>> gpurun_out/bench_fuse_$TAG.err || exit 1
+done
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$TAG -o run -- \
+    python -u $REPO/bench.py --steps 200 --no-cpu-baseline --no-traffic > $REPO/gpurun_out/bench_prof_$TAG.json \
+    2> $REPO/gpurun_out/bench_prof_$TAG.err
+rc=$?
+cd $REPO
+find /tmp/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/kstats_$TAG.csv \; 2>/dev/null
+echo "exit $rc"
+exit $rc

@@ -60,7 +60,7 @@ def gemm_indexed(Ah, X, ib, Rh, F, Ch, out):
     wsb = L.gnn_gemm_f32_split3_workspace_bytes(Rh, F, Ch, 1)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
     one = lambda p: (ctypes.c_void_p * 1)(p)
-    _lib.check(L.gnn_gemm_f32_split3_indexed(0, 1, Rh, F, Ch, 1, one(Ah.data_ptr()), Ah.stride(0), one(None), 0,
+    _lib.check(L.gnn_gemm_f32_split3_indexed(0, 1, Rh, F, Ch, 1, one(Ah.data_ptr()), Ah.stride(0), None, 0,
                                              one(X.data_ptr()), X.stride(0), one(ib.data_ptr()), X.shape[0],
                                              one(out.data_ptr()), out.stride(0), ws.data_ptr(), wsb,
                                              _lib.stream_of(dev)), "gnn_gemm_f32_split3_indexed")
@@ -140,7 +140,7 @@ def main():
     for li in (0, 1):
         L = hb.layers[li]
         # create_coo_tensor's values (cuda_spmm.cu:800): (1 / full degree of the row) * normfact[col]
-        deg = np.diff(L.fullrowptr).astype(np.float64)
+        deg = np.maximum(np.diff(L.fullrowptr), 1).astype(np.float64)  # (rows without entries: unused)
         r = np.repeat(np.arange(L.shape[0]), np.diff(L.rowptr))
         val = ((1.0 / deg)[r] * L.normfact.astype(np.float64)[L.colidx]).astype(np.float32)
         ops[li] = sp.csr_matrix((val, L.colidx, L.rowptr), shape=L.shape)

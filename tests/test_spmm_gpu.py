@@ -529,3 +529,69 @@ def test_create_coo_tensor_sums_duplicate_columns(dev):
     np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
     X = torch.randn(K, 40, device=dev)
     np.testing.assert_allclose(cso.spmm(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(), rtol=RTOL, atol=ATOL)
+
+
+# ---- small operands: spmm_row_kernel (a workgroup of WPR waves per (row, column slice)) ----
+def _layer2_like(rng, M, K, mean, max_len):
+    lens = powerlaw_lens(M, mean, 1.3, rng, K)
+    lens[:3] = [0, max_len, 1]  # an empty row, a hub row, a single entry
+    return random_csr(M, K, lens, rng)
+
+
+@pytest.mark.parametrize("wpr", ["1", "2", "4", "8", None])
+@pytest.mark.parametrize("shape", [(512, 8684, 1024, 29, 484), (8684, 512, 1024, 2, 40), (300, 700, 602, 30, 400),
+                                   (257, 300, 26, 12, 250), (64, 90, 7, 20, 90)])
+def test_row_kernel(dev, monkeypatch, wpr, shape):
+    """The layer-2-shaped calls (<= 64 k nonzeros) take spmm_row_kernel: vs the oracle within
+    1e-5; with one wave per row (WPR = 1) every output is the oracle's fmaf chain, bit for bit;
+    deterministic; the residual variant adds R[rmap[r]] in the row stores."""
+    M, K, F, mean, mx = shape
+    monkeypatch.setenv("GNN_SPMM_ROWK", "1")  # every form of the kernel (by default: short rows only)
+    if wpr is not None:
+        monkeypatch.setenv("GNN_SPMM_ROWK_WPR", wpr)
+    rng = np.random.default_rng(M + F)
+    full, rowptr, col, nf = _layer2_like(rng, M, K, mean, mx)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    cfg = cso.spmm_config(M, op.nnz, F, K=K)
+    assert cfg["kernel"].startswith("spmm_row_kernel"), cfg
+    if wpr is not None:
+        assert cfg["kernel"].endswith(f", {wpr}, false>"), cfg
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    Yref = O.spmm_f32(rowptr, ocol, oval, X)
+    Xd = torch.from_numpy(X).to(dev)
+    Y = cso.spmm_csr(op, Xd)
+    Y2 = cso.spmm_csr(op, Xd)
+    torch.cuda.synchronize()
+    assert torch.equal(Y, Y2), "deterministic"
+    if wpr == "1":
+        assert np.array_equal(Y.cpu().numpy(), Yref), "one wave per row: the oracle's fmaf chain"
+    np.testing.assert_allclose(Y.cpu().numpy(), Yref, rtol=RTOL, atol=ATOL)
+    # residual rows (the GraphSAGE input-gradient scatter, gnn_spmm_csr_f32_ex)
+    nres = max(1, M // 3)
+    R = rng.standard_normal((nres, F)).astype(np.float32)
+    rmap = np.full(M, -1, np.int32)
+    rmap[rng.choice(M, nres, replace=False)] = np.arange(nres, dtype=np.int32)
+    rmap[0] = 0  # the empty row gets a residual too
+    Yr = cso.spmm_csr(op, Xd, residual=torch.from_numpy(R).to(dev), rmap=torch.from_numpy(rmap).to(dev))
+    want = Yref.copy()
+    hit = rmap >= 0
+    want[hit] += R[rmap[hit]]
+    np.testing.assert_allclose(Yr.cpu().numpy(), want, rtol=RTOL, atol=ATOL)
+
+
+def test_row_kernel_off_matches(dev, monkeypatch):
+    """GNN_SPMM_ROWK=0 sends the same small call to the unit kernel: same result within 1e-5
+    (a short-row operand, the layer-2 backward's shape, which takes the row kernel by default)."""
+    rng = np.random.default_rng(11)
+    M, K, F = 8684, 512, 1024
+    full, rowptr, col, nf = _layer2_like(rng, M, K, 2, 40)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    X = torch.randn(K, F, device=dev)
+    assert cso.spmm_config(M, op.nnz, F, K=K)["kernel"] == "spmm_row_kernel<4, 4, 4, 1, false>"
+    a = cso.spmm_csr(op, X)
+    monkeypatch.setenv("GNN_SPMM_ROWK", "0")
+    assert cso.spmm_config(M, op.nnz, F, K=K)["kernel"].startswith("spmm_unit_kernel")
+    b = cso.spmm_csr(op, X)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=RTOL, atol=ATOL)
