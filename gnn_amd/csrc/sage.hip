@@ -151,6 +151,82 @@ __device__ __forceinline__ void grad_row(const GradSrc& s, int r, int lane, int 
   }
 }
 
+// The folded gradient's dependent chain, loaded one row ahead (AGG, split-row backward): the next
+// row's Aᵀ range and residual slot at the top of an iteration, its first two (col, val) at the end
+// (the range has arrived by then), so a row's own chain is only its G rows (+ the residual row).
+// The values travel in vector registers (lane 0 / 1 / 2: row start / end / residual slot; lane j <
+// 2: entry rb + j) and are read with readlane where used: vector loads retire in order, so using
+// them waits for nothing issued later (scalar loads may return out of order, and any use of one
+// waits for every scalar load in flight).
+struct Ahead {
+  int rv;    // lane 0: rb, lane 1: re, lane 2: q (rmap[r] or -1)
+  int cv;    // lane j < 2: col[rb + j]
+  float vv;  // lane j < 2: val[rb + j]
+};
+
+__device__ __forceinline__ int rdl(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ float rdlf(float x, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), l));
+}
+
+__device__ __forceinline__ void ahead_range(const GradSrc& s, int r, int M, int lane, Ahead& a) {
+  a.rv = lane == 2 ? -1 : 0;
+  if (r < M) {
+    if (lane < 2) a.rv = s.rp[r + lane];
+    else if (lane == 2 && s.rmap) a.rv = s.rmap[r];
+  }
+}
+
+__device__ __forceinline__ void ahead_pairs(const GradSrc& s, int lane, Ahead& a) {
+  const int rb = rdl(a.rv, 0), re = rdl(a.rv, 1);
+  const int e = rb + (lane & 1);
+  a.cv = 0;
+  a.vv = 0.0f;
+  if (lane < 2 && e < re) {
+    a.cv = s.col[e];
+    a.vv = s.val[e];
+  }
+}
+
+// The same values as grad_row<true>: the fmaf chain in CSR order from 0, then + the residual.
+template <int NV>
+__device__ __forceinline__ void grad_row_ahead(const GradSrc& s, const Ahead& a, int lane, int cbase, int cend,
+                                               f4 (&g)[NV]) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k) g[k] = f4(0.0f);
+  const int rb = rdl(a.rv, 0), re = rdl(a.rv, 1), q = rdl(a.rv, 2);
+  for (int e = rb; e < re; e += 2) {
+    const bool first = e == rb;  // wave-uniform
+    const bool two = e + 1 < re;
+    const int c0 = first ? rdl(a.cv, 0) : s.col[e];
+    const float v0 = first ? rdlf(a.vv, 0) : s.val[e];
+    const int c1 = first ? rdl(a.cv, 1) : (two ? s.col[e + 1] : 0);
+    const float v1 = first ? rdlf(a.vv, 1) : (two ? s.val[e + 1] : 0.0f);
+    const float* x0 = s.G + (int64_t)c0 * s.ldG;
+    const float* x1 = s.G + (int64_t)(two ? c1 : c0) * s.ldG;
+    f4 xs0[NV], xs1[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = cbase + (lane + 64 * k) * 4;
+      xs0[k] = c < cend ? *reinterpret_cast<const f4*>(x0 + c) : f4(0.0f);
+      xs1[k] = (two && c < cend) ? *reinterpret_cast<const f4*>(x1 + c) : f4(0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) g[k] = fma4(v0, xs0[k], g[k]);
+    if (two) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) g[k] = fma4(v1, xs1[k], g[k]);
+    }
+  }
+  if (q >= 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = cbase + (lane + 64 * k) * 4;
+      if (c < cend) g[k] += *reinterpret_cast<const f4*>(s.R + (int64_t)q * s.ldr + c);
+    }
+  }
+}
+
 template <int NV>
 __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restrict__ hB, int64_t ldb,
                                                             const float* __restrict__ bB, int D1,
@@ -305,6 +381,15 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
 // 3 workgroups per CU); the row sums meet in LDS (half 0 + half 1, fixed order) behind one
 // barrier per row pair, double-buffered by iteration parity.
 constexpr int BWD2_MAX_GRID = 1024;
+// The folded form (AGG) at 2,048 workgroups measured 36.7 vs 37.6 us for the kernel but +6 us of
+// finalize over twice the partial rows (profiles/round4/fold/, r4f): both forms keep 1,024;
+// GNN_SAGE_BWD2_GRID(_AGG) override it for sweeps (the workspace is sized for up to 2,048).
+constexpr int BWD2_GRID_SWEEP_MAX = 2048;
+int bwd2_grid_cap(bool agg) {
+  const char* e = std::getenv(agg ? "GNN_SAGE_BWD2_GRID_AGG" : "GNN_SAGE_BWD2_GRID");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 && v <= BWD2_GRID_SWEEP_MAX ? v : BWD2_MAX_GRID;
+}
 
 template <int NVH, bool AGG>
 __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
@@ -329,6 +414,11 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
     dbi[k] = f4(0.0f);
   }
   int it = 0;
+  Ahead nx{};  // AGG: the chain of this wave's next row, loaded one iteration ahead
+  if constexpr (AGG) {
+    ahead_range(src, blockIdx.x * 2 + slot, M, lane, nx);
+    ahead_pairs(src, lane, nx);
+  }
   for (int r0 = blockIdx.x * 2; r0 < M; r0 += gridDim.x * 2, ++it) {
     const int r = r0 + slot;
     const bool live = r < M;
@@ -336,17 +426,24 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
     float a = 0.0f, b = 0.0f;
     float m = 0.0f, rs = 0.0f;
     f4 hv[NVH];
+    Ahead cur{};
+    if constexpr (AGG) cur = nx;
     if (live) {
       m = mean[r];
       rs = rstd[r];
-      // the row's pre-activations first: their loads overlap the gradient's dependent chain
-      // (Aᵀ row pointer -> (col, val) -> G rows) when the gradient is aggregated here
+      // the row's pre-activations first: their loads overlap the gradient's G-row loads
 #pragma unroll
       for (int k = 0; k < NVH; ++k) {
         const int c = cbase + (lane + 64 * k) * 4;
         hv[k] = c < cend ? load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c) : f4(0.0f);
       }
-      grad_row<AGG, NVH>(src, r, lane, cbase, cend, gx);  // the output gradient, scaled below
+    }
+    if constexpr (AGG) ahead_range(src, r + gridDim.x * 2, M, lane, nx);  // the next row's range
+    if (live) {
+      if constexpr (AGG)
+        grad_row_ahead<NVH>(src, cur, lane, cbase, cend, gx);  // the output gradient, scaled below
+      else
+        grad_row<false, NVH>(src, r, lane, cbase, cend, gx);
     }
 #pragma unroll
     for (int k = 0; k < NVH; ++k) {
@@ -400,6 +497,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
         }
       }
     }
+    if constexpr (AGG) ahead_pairs(src, lane, nx);  // the next row's first (col, val) pairs (its range is here)
   }
   // workgroup column sums -> partial[blockIdx.x][q][D]: slot 0 + slot 1 (fixed order)
 #pragma unroll
@@ -499,8 +597,8 @@ BwdFn bwd2_fn(int nvh) {
 // the split-row form applies (and its grid G, which sizes the partial slab)
 bool use_bwd2(int64_t D) { return D % 8 == 0 && D >= 512 && std::getenv("GNN_SAGE_BWD1") == nullptr; }
 
-int64_t bwd_grid(int64_t M, int64_t D) {
-  if (use_bwd2(D)) return std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 2), BWD2_MAX_GRID));
+int64_t bwd_grid(int64_t M, int64_t D, bool agg = false) {
+  if (use_bwd2(D)) return std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 2), bwd2_grid_cap(agg)));
   const int64_t cap = bwd_grid_cap();
   return std::max<int64_t>(1, ceil_div(M, 4) < cap ? ceil_div(M, 4) : cap);
 }
@@ -559,7 +657,10 @@ int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float*
 }
 
 size_t gnn_sage_norm_bwd_workspace_bytes(int64_t M, int64_t D) {
-  const int64_t G = M <= 0 ? 1 : bwd_grid(M, D);
+  // sized for the largest grid a sweep may ask for
+  const int64_t G = M <= 0 ? 1 : (use_bwd2(D) ? std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 2),
+                                                                                        BWD2_GRID_SWEEP_MAX))
+                                              : bwd_grid(M, D));
   return gnn::align_up((size_t)G * NRED * (size_t)(D > 0 ? D : 1) * sizeof(float), 256);
 }
 
@@ -593,7 +694,7 @@ int sage_norm_bwd(const GradSrc& src, bool agg, const float* hB, int64_t ldb, in
   GNN_REQUIRE(D2 == 0 || (uintptr_t)dhW % 16 == 0, "gnn_sage_norm_bwd_f32: dhW not 16-byte aligned");
   GNN_REQUIRE(workspace && workspace_bytes >= gnn_sage_norm_bwd_workspace_bytes(M, D),
               "gnn_sage_norm_bwd_f32: workspace too small");
-  const int64_t G = bwd_grid(M, D);
+  const int64_t G = bwd_grid(M, D, agg);
   const float inv_keep = 1.0f / (1.0f - p_drop);
   float* partial = (float*)workspace;
   if (use_bwd2(D)) {
