@@ -160,7 +160,7 @@ struct WorkMap {
 // One column chunk per lane: held to 8 waves per SIMD (<= 64 VGPRs; the slot-skip branches
 // below otherwise take 66); wider instantiations keep the compiler's choice (no spills).
 template <int VW, int G, int NJ, int U, bool RES>
-__global__ __launch_bounds__(256, NJ == 1 ? 8 : 1) void spmm_unit_kernel(
+__global__ __launch_bounds__(256, (NJ == 1 && U <= 4) ? 8 : 1) void spmm_unit_kernel(
     const int* __restrict__ rowptr, const int* __restrict__ col, const float* __restrict__ val,
     int M, int nnz, int S, int nunits,
     const float* __restrict__ X, int64_t ldx,
@@ -1194,6 +1194,9 @@ struct SpmmCfg {
   // small operands: spmm_row_kernel<vw, rnj, ru, wpr> over M * slices workgroups (wpr == 0: the
   // unit kernel above)
   int wpr, rnj, ru, slices;
+  // small operands cut into 256-float column tiles (small_tiles): 16 nonzeros in flight per lane
+  // instead of 4 (their units are short chains of latency-bound rounds)
+  bool u16;
 };
 
 // The row kernel takes operands whose nonzeros are too few to fill the chip with units: up to
@@ -1320,12 +1323,15 @@ SpmmCfg make_cfg(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int6
     }
   }
   // Small operands: 256-float column tiles (G = 64, one chunk) for parallelism (small_tiles).
+  c.u16 = false;
   if (c.vw == 4 && c.tiles == 1) {
     const int64_t t = small_tiles(M, nnz, F);
     if (t > 1) {
       c.g = 64;
       c.nj = 1;
       c.tiles = (int)ceil_div(F, (int64_t)256);
+      const char* e = getenv("GNN_SPMM_SMALL_U16");  // A/B
+      c.u16 = !(e && atoi(e) == 0);
     }
   }
   // Experiment override (benchmarks only): GNN_SPMM_G / GNN_SPMM_NJ force the lane group
@@ -1403,6 +1409,8 @@ MainFn main_by_g(int g, int nj, bool res) {
 // res: the row-mapped residual variant (gnn_spmm_csr_f32_ex); a separate instantiation, so
 // the plain aggregation carries no residual code and the two show up apart in rocprofv3.
 MainFn select_main(const SpmmCfg& c, bool res) {
+  if (c.u16 && c.vw == 4 && c.g == 64 && c.nj == 1)
+    return res ? &spmm_unit_kernel<4, 64, 1, 16, true> : &spmm_unit_kernel<4, 64, 1, 16, false>;
   switch (c.vw) {
     case 4: return main_by_g<4>(c.g, c.nj, res);
     case 2: return main_by_g<2>(c.g, c.nj, res);
@@ -1442,7 +1450,8 @@ std::string main_kernel_name(const SpmmCfg& c, bool res) {
   if (c.wpr)
     snprintf(b, sizeof b, "spmm_row_kernel<%d, %d, %d, %d, %s>", c.vw, c.rnj, c.ru, c.wpr, res ? "true" : "false");
   else
-    snprintf(b, sizeof b, "spmm_unit_kernel<%d, %d, %d, %d, %s>", c.vw, c.g, c.nj, pick_u(c.nj), res ? "true" : "false");
+    snprintf(b, sizeof b, "spmm_unit_kernel<%d, %d, %d, %d, %s>", c.vw, c.g, c.nj,
+             (c.u16 && c.vw == 4 && c.g == 64 && c.nj == 1) ? 16 : pick_u(c.nj), res ? "true" : "false");
   return b;
 }
 

@@ -107,7 +107,8 @@ def test_workspace_and_config():
     # the main kernel each call launches: the layer-2 calls (<= 64 k nonzeros) take the row kernel
     # (a workgroup per (row, slice), no combine), the big layers the unit kernel; a fixed unit
     # size always asks for the unit kernel
-    assert spmm_config(512, 14876, 1024, K=8680)["kernel"] == "spmm_unit_kernel<4, 64, 1, 4, false>"  # long rows
+    # long rows: the unit kernel, 256-float tiles, 16 nonzeros in flight per lane
+    assert spmm_config(512, 14876, 1024, K=8680)["kernel"] == "spmm_unit_kernel<4, 64, 1, 16, false>"
     assert spmm_config(8680, 14876, 1024, K=512)["kernel"] == "spmm_row_kernel<4, 4, 4, 1, false>"
     assert spmm_config(8680, 14876, 1024, K=512, unit_nnz=4)["kernel"].startswith("spmm_unit_kernel<4, 64, 4")
     assert spmm_config(15768, 1821171, 604, K=22153, ldx=604, ldy=604)["kernel"] == \
