@@ -92,18 +92,20 @@ bool fills(int64_t M, int64_t N, int n) { return ceil_div(M, 128) * ceil_div(N, 
 bool gemm_ok(const void* p, int64_t ld) { return ((uintptr_t)p % 8) == 0 && (ld % 2) == 0; }
 
 std::mutex g_blas_mu;
-rocblas_handle g_blas[64] = {};
+rocblas_handle g_blas[64][2] = {};
 
-int blas_handle(rocblas_handle* h) {
+// which = 0: the step's stream; 1: the aux stream (its own handle, so the two streams' small
+// products never share a handle's workspace)
+int blas_handle(rocblas_handle* h, int which = 0) {
   int dev = 0;
   GNN_HIP(hipGetDevice(&dev), "hipGetDevice");
   GNN_REQUIRE(dev >= 0 && dev < 64, "gnn_train_step: device index %d", dev);
   std::lock_guard<std::mutex> g(g_blas_mu);
-  if (!g_blas[dev]) {
-    if (rocblas_create_handle(&g_blas[dev]) != rocblas_status_success)
+  if (!g_blas[dev][which]) {
+    if (rocblas_create_handle(&g_blas[dev][which]) != rocblas_status_success)
       return gnn::fail(-1, "rocblas_create_handle failed");
   }
-  *h = g_blas[dev];
+  *h = g_blas[dev][which];
   return 0;
 }
 
@@ -187,6 +189,16 @@ size_t gemm_ws(int64_t M, int64_t N, int64_t K, int nb) {
 // it into the layer-1 tail backward (A/B; the values are bit-identical either way)
 bool fuse_agg_enabled() {
   const char* e = getenv("GNN_STEP_FUSE_AGG");  // read per step (tests toggle it in-process)
+  return !(e && atoi(e) == 0);
+}
+
+// GNN_STEP_SMALL_OVERLAP=0 keeps everything on the step's stream. By default the top layer's
+// small, latency-bound pieces that do not depend on each other run on the aux stream: in the
+// forward x[sampled] + linearB beside the aggregation + linearW; in the backward the head's and
+// the top layer's weight gradients beside the input gradients and the layer below (same kernels,
+// same handles' results: bit-identical).
+bool small_overlap_enabled() {
+  const char* e = getenv("GNN_STEP_SMALL_OVERLAP");
   return !(e && atoi(e) == 0);
 }
 
@@ -377,10 +389,17 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
   }();
   const int training = (int)d[GNN_SH_TRAINING];
   Aux* aux = nullptr;
-  if (overlap_enabled() && !f32_gemm()) GNN_TRY(aux_of(st, &aux));
+  const bool big_ov = overlap_enabled() && !f32_gemm();  // the big layers' GEMMs beside their SpMMs (off)
+  const bool small_ov = small_overlap_enabled();
+  if (big_ov || small_ov) GNN_TRY(aux_of(st, &aux));
   std::unique_lock<std::mutex> aux_lock;
   if (aux) aux_lock = std::unique_lock<std::mutex>(aux->mu);
   bool aux_used = false;
+  rocblas_handle ha = nullptr;  // the aux stream's handle (small products there)
+  if (aux && small_ov) {
+    GNN_TRY(blas_handle(&ha, 1));
+    if (rocblas_set_stream(ha, aux->s) != rocblas_status_success) return gnn::fail(-1, "rocblas_set_stream failed");
+  }
   // optional per-aggregation timing (GNN_SH_TIMING): arm the caller's event pair for the next
   // SpMM launch (gnn_spmm_set_timing_events) and record the call's shape beside it
   int64_t* const T = HP<int64_t>(d, GNN_SH_TIMING);
@@ -403,7 +422,9 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_REQUIRE(L(d, l, GNN_SL_NSAMPLED) == b.M, "gnn_train_step: layer %d sampled %lld != M %lld", l,
                   (long long)L(d, l, GNN_SL_NSAMPLED), (long long)b.M);
     const bool ok = gemm_ok(b.feat, b.ldo) && gemm_ok(WW, b.F) && (!pl.sage || gemm_ok(WB, b.F));
-    if (aux && pl.sage && ok && fills(b.M, N, n)) {
+    // the top layer's small products (rocBLAS): x[sampled] + linearB on the aux stream beside A·X
+    const bool small_side = ha && pl.sage && !(ok && fills(b.M, N, n));
+    if (big_ov && pl.sage && ok && fills(b.M, N, n)) {
       // x[sampled] and linearB on the aux stream beside A·X and linearW; each product launched
       // alone with the split choice of the pair, so the sums are those of the batched launch
       b.xs_gathered = true;
@@ -424,6 +445,18 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       float* Cw[1] = {b.hW};
       GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, Aw, b.ldo, Bw, b.F, Cw, N, b.ws_gemm_f, b.b_gemm_f, st));
       GNN_TRY(fork_join(aux, aux->s, st));
+    } else if (small_side) {
+      b.xs_gathered = true;
+      GNN_TRY(fork_join(aux, st, aux->s));  // aux sees X complete
+      GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M,
+                                  b.F, aux->s));
+      GNN_TRY(mm_xwt(ha, b.xs, b.ldo, WB, b.F, b.hB, N, b.M, N, b.F));
+      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                               b.ws_fwd, b.b_fwd, 0, st));
+      GNN_TRY(mm_xwt(h, b.feat, b.ldo, WW, b.F, b.hW, N, b.M, N, b.F));
+      GNN_TRY(fork_join(aux, aux->s, st));  // the tail reads hB
     } else {
       arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
@@ -437,7 +470,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
         GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M,
                                     b.F, st));
     }
-    if (aux && pl.sage && ok && fills(b.M, N, n)) {
+    if ((big_ov && pl.sage && ok && fills(b.M, N, n)) || small_side) {
       // done above
     } else if (ok && fills(b.M, N, n) && !b.xs_gathered) {
       const float* A[2] = {b.X, b.feat};
@@ -472,10 +505,19 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
   // ------------------------------------------------------------------ backward
   GNN_TRY(gnn_head_bce_bwd_f32(top.Y, top.D, pl.Mh, pl.Dh, Wh, pl.C, labels, ldl, nullptr, p, hseed, training, pl.z,
                                pl.nrm, pl.dz, pl.dXh, pl.Dh, st));
-  GNN_TRY(mm_gtx(h, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
+  // the head's weight and bias gradients: on the aux stream beside the top layer's backward
+  hipStream_t shead = st;
+  rocblas_handle hhead = h;
+  if (ha) {
+    GNN_TRY(fork_join(aux, st, aux->s));
+    shead = aux->s;
+    hhead = ha;
+    aux_used = true;
+  }
+  GNN_TRY(mm_gtx(hhead, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
   if (HP<float>(d, GNN_SH_HEAD_GB)) {
-    colsum_kernel<<<dim3((unsigned)pl.C), dim3(256), 0, st>>>(pl.dz, (int)pl.Mh, (int)pl.C,
-                                                            HP<float>(d, GNN_SH_HEAD_GB));
+    colsum_kernel<<<dim3((unsigned)pl.C), dim3(256), 0, shead>>>(pl.dz, (int)pl.Mh, (int)pl.C,
+                                                               HP<float>(d, GNN_SH_HEAD_GB));
     GNN_LAUNCHED("colsum_kernel");
   }
   // gradient-ready events (GNN_SH_GRAD_EVENTS): the caller's DP exchange of a bucket starts there
@@ -484,7 +526,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     if (E && slot < E[0] && E[slot]) GNN_HIP(hipEventRecord((hipEvent_t)E[slot], s), "hipEventRecord (grad event)");
     return 0;
   };
-  GNN_TRY(grads_ready(1, st));
+  GNN_TRY(grads_ready(1, shead));
   for (int l = pl.nl - 1; l >= 0; --l) {
     LayerBufs& b = pl.lb[l];
     const int64_t N = b.N;
@@ -530,7 +572,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       const int64_t* IB[2] = {pl.sage && !b.xs_gathered ? P<const int64_t>(d, l, GNN_SL_SAMPLED) : nullptr, nullptr};
       float* Cc[2] = {pl.sage ? gWB : gWW, gWW};
       hipStream_t sw = st;
-      if (aux && l >= 1) {
+      if (big_ov && l >= 1) {
         GNN_TRY(fork_join(aux, st, aux->s));
         sw = aux->s;
         aux_used = true;
@@ -543,9 +585,19 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
                                     b.b_gemm_dw, sw));
       GNN_TRY(grads_ready(2 + l, sw));  // sw follows st's norm backward (fork_join)
     } else {
-      if (pl.sage) GNN_TRY(mm_gtx(h, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
-      GNN_TRY(mm_gtx(h, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
-      GNN_TRY(grads_ready(2 + l, st));
+      // the small weight-gradient products (rocBLAS): on the aux stream beside the input gradients
+      // and the layer below (their inputs are final: the norm backward and x[sampled] / A·X)
+      hipStream_t sw = st;
+      rocblas_handle hw = h;
+      if (ha) {
+        GNN_TRY(fork_join(aux, st, aux->s));
+        sw = aux->s;
+        hw = ha;
+        aux_used = true;
+      }
+      if (pl.sage) GNN_TRY(mm_gtx(hw, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
+      GNN_TRY(mm_gtx(hw, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
+      GNN_TRY(grads_ready(2 + l, sw));
     }
     if (l >= 1) {  // dY_{l-1} = A_lᵀ·dfeat (+ dxs through rmap: the x[sampled] gradient)
       LayerBufs& prev = pl.lb[l - 1];

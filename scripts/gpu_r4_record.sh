@@ -1,0 +1,27 @@
+# Round-4 GPU record on the final tree: the whole GPU suite, smoke, the default bench (PMC traffic +
+# CPU baseline), the config-1 CPU bench, the default bench under rocprofv3 kernel stats, and the
+# self-launched N = 2 rehearsal (both ranks on the one GPU over gloo; RCCL refuses two ranks on one GPU).
+# Usage: bash scripts/gpu_r4_record.sh TAG
+set -o pipefail
+TAG=${1:-r4rec}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+REPO=$(pwd)
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > gpurun_out/gputest_$TAG.log 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 && \
+timeout -k 10 600 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err && \
+timeout -k 10 300 python -u bench.py --cpu --steps 30 --warmup 3 > gpurun_out/bench_cpu_cfg1_$TAG.json \
+    2> gpurun_out/bench_cpu_cfg1_$TAG.err && \
+GNN_DIST_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 20 --warmup 3 \
+    > gpurun_out/bench_selflaunch2_$TAG.json 2> gpurun_out/bench_selflaunch2_$TAG.err && \
+GNN_DIST_BACKEND=gloo timeout -k 10 500 python3 bench.py --gpus 4 --steps 20 --warmup 3 \
+    > gpurun_out/bench_selflaunch4_$TAG.json 2> gpurun_out/bench_selflaunch4_$TAG.err && \
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_$TAG -o run -- \
+    python -u $REPO/bench.py --no-cpu-baseline --no-traffic > $REPO/gpurun_out/bench_prof_$TAG.json \
+    2> $REPO/gpurun_out/bench_prof_$TAG.err
+rc=$?
+cd $REPO
+find /tmp/prof_$TAG -name "*kernel_stats.csv" -exec cp {} gpurun_out/kstats_$TAG.csv \; 2>/dev/null
+echo "exit $rc"
+exit $rc

@@ -1,0 +1,58 @@
+"""CPU: bench.py's per-call-site roofline bookkeeping (roofline_from) over timing records as the
+native executor names them (fwd_L0, fwd_L1, fwd_L2, bwd_L1: the layer-2 backward folded into the
+layer-1 tail leaves no record) and as the autograd path emits them (fwd / bwd, five per step in
+call order): every record lands on its call site and its own step's batch."""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+from gnn_amd.sampler import HostLayer  # noqa: E402
+
+
+class _HB:
+    def __init__(self, seed):
+        rng = np.random.default_rng(seed)
+        self.layers = []
+        for M, K in ((30, 40), (20, 30), (5, 20)):
+            rowptr = np.concatenate([[0], np.cumsum(rng.integers(0, 4, M))]).astype(np.int32)
+            colidx = np.sort(rng.integers(0, K, rowptr[-1])).astype(np.int32)
+            self.layers.append(HostLayer(fullrowptr=rowptr, rowptr=rowptr, colidx=colidx,
+                                         normfact=np.ones(K, np.float32), shape=(M, K)))
+
+
+def _rec(tag, li, hb, F, kname):
+    L = hb.layers[li]
+    M, K = L.shape if tag.startswith("fwd") else L.shape[::-1]
+    nnz = L.nnz
+    return (tag, 0.01, nnz * F * 4 + nnz * 8 + (M + 1) * 4 + M * F * 4, kname,
+            dict(M=M, K=K, nnz=nnz, F=F, res_rows=0))
+
+
+def test_roofline_from_executor_tags_and_positional():
+    hbs = [_HB(s) for s in range(3)]
+    batches = [(hb, None) for hb in hbs]
+
+    class A:
+        pass
+
+    # executor: four named records per step (the folded bwd_L2 has none)
+    recs = []
+    for hb in hbs:
+        for tag, li in (("fwd_L0", 0), ("fwd_L1", 1), ("fwd_L2", 2), ("bwd_L1", 1)):
+            recs.append(_rec(tag, li, hb, 8, "k_big" if li < 2 else "k_small"))
+    roof, detail = bench.roofline_from(recs, batches, A(), None, len(hbs))
+    assert sorted(detail) == ["bwd_L1", "fwd_L0", "fwd_L1", "fwd_L2"]
+    assert roof["kernel"].startswith("k_big") and "over 9 launches" in roof["kernel"]
+    # autograd path: five unnamed records per step in call order
+    recs = []
+    for hb in hbs:
+        for tag, li in (("fwd", 0), ("fwd", 1), ("fwd", 2), ("bwd", 2), ("bwd", 1)):
+            recs.append(_rec(tag, li, hb, 8, "k_big" if li < 2 else "k_small"))
+    roof, detail = bench.roofline_from(recs, batches, A(), None, len(hbs))
+    assert sorted(detail) == ["bwd_L1", "bwd_L2", "fwd_L0", "fwd_L1", "fwd_L2"]
+    assert "over 9 launches" in roof["kernel"]

@@ -595,3 +595,35 @@ def test_row_kernel_off_matches(dev, monkeypatch):
     b = cso.spmm_csr(op, X)
     torch.cuda.synchronize()
     np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=RTOL, atol=ATOL)
+
+
+def test_small_tiled_unit_kernel_u16(dev, monkeypatch):
+    """The layer-2 forward's shape (512 long-tailed rows, ~15 k nonzeros, F = 1024) runs the unit
+    kernel in 256-float column tiles with 16 nonzeros in flight per lane: vs the oracle within
+    1e-5, with and without the residual, and bit-identical to 4 in flight (GNN_SPMM_SMALL_U16=0:
+    one lane group per row, the same per-lane fmaf order)."""
+    rng = np.random.default_rng(23)
+    M, K, F = 512, 8684, 1024
+    full, rowptr, col, nf = _layer2_like(rng, M, K, 29, 484)
+    op = _op(dev, full, rowptr, col, nf, M, K)
+    assert cso.spmm_config(M, op.nnz, F, K=K)["kernel"] == "spmm_unit_kernel<4, 64, 1, 16, false>"
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    Yref = O.spmm_f32(rowptr, ocol, oval, X)
+    Xd = torch.from_numpy(X).to(dev)
+    Y16 = cso.spmm_csr(op, Xd)
+    R = torch.randn(100, F, device=dev)
+    rmap = torch.full((M,), -1, dtype=torch.int32, device=dev)
+    rmap[torch.randperm(M, device=dev)[:100]] = torch.arange(100, dtype=torch.int32, device=dev)
+    Yr16 = cso.spmm_csr(op, Xd, residual=R, rmap=rmap)
+    monkeypatch.setenv("GNN_SPMM_SMALL_U16", "0")
+    assert cso.spmm_config(M, op.nnz, F, K=K)["kernel"] == "spmm_unit_kernel<4, 64, 1, 4, false>"
+    Y4 = cso.spmm_csr(op, Xd)
+    Yr4 = cso.spmm_csr(op, Xd, residual=R, rmap=rmap)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Y16.cpu().numpy(), Yref, rtol=RTOL, atol=ATOL)
+    assert torch.equal(Y16, Y4) and torch.equal(Yr16, Yr4)
+    want = torch.from_numpy(Yref).to(dev)
+    hit = rmap >= 0
+    want[hit] += R[rmap[hit].long()]
+    np.testing.assert_allclose(Yr16.cpu().numpy(), want.cpu().numpy(), rtol=RTOL, atol=ATOL)
