@@ -63,6 +63,10 @@ _SIGNATURES = {
     "gnn_sage_norm_bwd_agg_f32": (_INT, [_VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _I64, _I64, _VP, _I64, _I64,
                                          _VP, _VP, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_uint64, _INT, _VP,
                                          _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    "gnn_gemm_p3_packed_bytes": (_SZ, [_I64, _I64]),
+    "gnn_gemm_p3_pack_f32": (_INT, [_VP, _I64, _INT, _VP, _I64, _I64, _VP, _SZ, _VP]),
+    "gnn_gemm_p3_workspace_bytes": (_SZ, [_I64, _I64, _I64, _INT]),
+    "gnn_gemm_p3": (_INT, [_I64, _I64, _I64, _INT, _VP, _VP, _VP, _I64, _VP, _SZ, _VP]),
     # include/gnn_optim.h
     "gnn_optim_chunks": (_I64, [_INT, _VP]),
     "gnn_grad_sqnorm_f32": (_INT, [_INT, _VP, _VP, _VP, _VP]),

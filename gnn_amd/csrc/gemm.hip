@@ -567,6 +567,181 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
 }
 
+// ---------------------------------------------------------------------------------
+// "p3": split3 on operands split ONCE into their three bf16 pieces in HBM (gnn_gemm_p3_pack_f32)
+// instead of in every workgroup's registers. The split3 kernel spends ~3 of its ~5 vector
+// instructions per MFMA on the split (and/sub/perm), and it is bound by the SIMD's issue port
+// (profiles/round1/gemm_split3_pmc_summary.txt: MFMA busy 0.42-0.51, issue stalls 0.45-0.53); a
+// packed operand costs 1.5x the fp32 bytes per tile but no vector work. Packed layout (per
+// operand, viewed as R rows — M for A, N for B — by K): three planes [piece][k tile][R_pad][16]
+// bf16, rows and k zero-padded to 128 / 16, so a thread's 16 bytes of (row, k half) are one
+// coalesced load and the GEMM needs no guards. The pieces are the split3 kernel's (truncation,
+// exact) and the MFMA schedule is the same (same k16 steps, same six products in the same
+// order): results bit-identical to gnn_gemm_f32_split3.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void split_piece8(const float v[8], u4v& ph, u4v& pm, u4v& pl) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 x = f2{v[2 * j], v[2 * j + 1]};
+    const unsigned int h0 = __float_as_uint(x.x) & 0xffff0000u, h1 = __float_as_uint(x.y) & 0xffff0000u;
+    const f2 r = x - f2{__uint_as_float(h0), __uint_as_float(h1)};
+    const unsigned int m0 = __float_as_uint(r.x) & 0xffff0000u, m1 = __float_as_uint(r.y) & 0xffff0000u;
+    const f2 l = r - f2{__uint_as_float(m0), __uint_as_float(m1)};
+    ph[j] = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
+    pm[j] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+    pl[j] = __builtin_amdgcn_perm(__float_as_uint(l.y), __float_as_uint(l.x), 0x07060302u);
+  }
+}
+
+// One (128-row block, k tile) per workgroup. m-major source (element (r, k) = src[row(r)*ld + k]):
+// thread t takes row t >> 1, k half t & 1; k-major source (element (r, k) = src[row(k)*ld + r]):
+// row t & 127, the wave-uniform k half t >> 7 (each of the 8 loads is one coalesced k row).
+// idx (optional): the source's row index (r for m-major, k for k-major).
+__global__ __launch_bounds__(256) void p3_pack_kernel(const float* __restrict__ src, int64_t ld, int kmajor,
+                                                      const int64_t* __restrict__ idx, int R, int K, int Rp, int KT,
+                                                      unsigned short* __restrict__ out) {
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * 128;
+  const int kt = blockIdx.y;
+  const int rr = kmajor ? (t & 127) : (t >> 1);
+  const int kh = kmajor ? (t >> 7) : (t & 1);
+  const int r = r0 + rr;
+  const int kb = kt * 16 + kh * 8;
+  float v[8];
+  if (!kmajor) {
+    const float* q = (r < R) ? src + (idx ? idx[r] : (int64_t)r) * ld : nullptr;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (q && kb + i < K) ? q[kb + i] : 0.0f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = kb + i;
+      v[i] = (r < R && k < K) ? src[(idx ? idx[k] : (int64_t)k) * ld + r] : 0.0f;
+    }
+  }
+  u4v ph, pm, pl;
+  split_piece8(v, ph, pm, pl);
+  const int64_t plane = (int64_t)KT * Rp * 16;
+  const int64_t o = ((int64_t)kt * Rp + r) * 16 + kh * 8;
+  *reinterpret_cast<u4v*>(out + o) = ph;
+  *reinterpret_cast<u4v*>(out + plane + o) = pm;
+  *reinterpret_cast<u4v*>(out + 2 * plane + o) = pl;
+}
+
+struct PBatch {
+  const unsigned short* A[MAX_BATCH];
+  const unsigned short* B[MAX_BATCH];
+  float* C[MAX_BATCH];
+};
+
+// The split3 kernel's tile, pipeline and MFMA schedule over packed operands: 3 x 16 bytes per
+// operand per thread per k tile (one per piece) straight into the LDS images (m-major form).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_p3_kernel(
+    PBatch bt, int M, int N, int Mp, int Np, int KT, int64_t ldc, int splits, int ktlen, float* __restrict__ part,
+    int xcd_map) {
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][S3_OPER];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (xcd_map) {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int per = total >> 3;
+    const int lg = hw < per * 8 ? (hw & 7) * per + (hw >> 3) : hw;
+    tx = lg % gx;
+    ty = (lg / gx) % gy;
+    tz = lg / (gx * gy);
+  }
+  const int b = tz / splits;
+  const int split = tz % splits;
+  const int m0 = ty * BM;
+  const int n0 = tx * BN;
+  const int ktb = split * ktlen;
+  const int kte = min(KT, ktb + ktlen);
+  const int64_t aplane = (int64_t)KT * Mp * 16, bplane = (int64_t)KT * Np * 16;  // bf16 units
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)bt.A[b], (short)0,
+                                                                      (int)(3 * aplane * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)bt.B[b], (short)0,
+                                                                      (int)(3 * bplane * 2), 0x00020000);
+  const int rr = t >> 1, kh = t & 1;
+  const int voa = ((m0 + rr) * 16 + kh * 8) * 2, vob = ((n0 + rr) * 16 + kh * 8) * 2;  // bytes
+  const int off = s3_chunk<false>(rr, kh);
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f16v(0.0f);
+
+  u4v ra[2][3], rb[2][3];
+  const int nfull = kte - ktb;
+  auto load_ab = [&](int kt, u4v(&xa)[3], u4v(&xb)[3]) {
+    const int k = ktb + min(kt, nfull - 1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      xa[p] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rsa, voa, (int)((p * aplane + (int64_t)k * Mp * 16) * 2), 0));
+      xb[p] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                          rsb, vob, (int)((p * bplane + (int64_t)k * Np * 16) * 2), 0));
+    }
+  };
+  auto store_ab = [&](int stage, const u4v(&xa)[3], const u4v(&xb)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<u4v*>(As[stage] + p * S3_PIECE + off) = xa[p];
+      *reinterpret_cast<u4v*>(Bs[stage] + p * S3_PIECE + off) = xb[p];
+    }
+  };
+  const int li = lane & 31, lh = lane >> 5;
+  if (nfull > 0) {
+    load_ab(0, ra[0], rb[0]);
+    load_ab(1, ra[1], rb[1]);
+    store_ab(0, ra[0], rb[0]);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nfull; kt += 2) {
+      load_ab(kt + 2, ra[0], rb[0]);
+      s3_mma<false, false>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      store_ab(1, ra[1], rb[1]);
+      __syncthreads();
+      load_ab(kt + 3, ra[1], rb[1]);
+      s3_mma<false, false>(As[1], Bs[1], wm * 64, wn * 64, li, lh, acc);
+      store_ab(0, ra[0], rb[0]);
+      __syncthreads();
+    }
+    if (nfull & 1) {
+      s3_mma<false, false>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
+      __syncthreads();
+    }
+  }
+  float* __restrict__ Cb;
+  int64_t ldo;
+  if (splits > 1) {
+    Cb = part + (int64_t)tz * M * N;
+    ldo = N;
+  } else {
+    Cb = bt.C[b];
+    ldo = ldc;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + li;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cb[(int64_t)m * ldo + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // Workgroup slots of the chip at each kernel's occupancy: f32-input kernel 2 per CU (80 KB of
 // LDS each), split3 kernel 3 per CU (48 KB).
 constexpr int64_t SLOTS_F32 = 2 * 256;
@@ -720,6 +895,82 @@ int gnn_gemm_f32(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, in
                  size_t workspace_bytes, void* stream) {
   return gemm_run(ALGO_F32, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
                   stream);
+}
+
+size_t gnn_gemm_p3_packed_bytes(int64_t R, int64_t K) {
+  if (R <= 0 || K <= 0) return 0;
+  return (size_t)3 * (size_t)ceil_div(K, (int64_t)16) * (size_t)(ceil_div(R, (int64_t)128) * 128) * 16 * 2;
+}
+
+int gnn_gemm_p3_pack_f32(const float* src, int64_t ld, int kmajor, const int64_t* idx, int64_t R, int64_t K,
+                         void* out, size_t out_bytes, void* stream) {
+  GNN_REQUIRE(R >= 0 && K >= 0 && R < INT_MAX && K < INT_MAX, "gnn_gemm_p3_pack_f32: bad size");
+  if (R == 0 || K == 0) return 0;
+  GNN_REQUIRE(src && out, "gnn_gemm_p3_pack_f32: NULL pointer");
+  GNN_REQUIRE(out_bytes >= gnn_gemm_p3_packed_bytes(R, K), "gnn_gemm_p3_pack_f32: output too small");
+  GNN_REQUIRE((uintptr_t)out % 16 == 0, "gnn_gemm_p3_pack_f32: output not 16-byte aligned");
+  GNN_REQUIRE(gnn_gemm_p3_packed_bytes(R, K) < (size_t)INT_MAX, "gnn_gemm_p3_pack_f32: packed operand >= 2 GiB");
+  const int Rp = (int)(ceil_div(R, (int64_t)128) * 128), KT = (int)ceil_div(K, (int64_t)16);
+  p3_pack_kernel<<<dim3((unsigned)(Rp / 128), (unsigned)KT), dim3(256), 0, (hipStream_t)stream>>>(
+      src, ld, kmajor, idx, (int)R, (int)K, Rp, KT, (unsigned short*)out);
+  GNN_LAUNCHED("p3_pack_kernel");
+  return 0;
+}
+
+size_t gnn_gemm_p3_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch) {
+  return workspace_bytes_of(ALGO_S3, M, N, K, nbatch);
+}
+
+int gnn_gemm_p3(int64_t M, int64_t N, int64_t K, int nbatch, const void* const* Ap, const void* const* Bp,
+                float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+  GNN_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M < INT_MAX && N < INT_MAX && K < INT_MAX, "gnn_gemm_p3: bad size");
+  GNN_REQUIRE(nbatch >= 1 && nbatch <= MAX_BATCH, "gnn_gemm_p3: nbatch must be 1..%d", MAX_BATCH);
+  if (M == 0 || N == 0) return 0;
+  GNN_REQUIRE(Ap && Bp && C && ldc >= N, "gnn_gemm_p3: NULL pointer array or ldc < N");
+  PBatch bt{};
+  for (int b = 0; b < nbatch; ++b) {
+    GNN_REQUIRE(C[b] && (K == 0 || (Ap[b] && Bp[b])), "gnn_gemm_p3: NULL operand %d", b);
+    GNN_REQUIRE((uintptr_t)Ap[b] % 16 == 0 && (uintptr_t)Bp[b] % 16 == 0, "gnn_gemm_p3: packed operands 16-byte aligned");
+    bt.A[b] = (const unsigned short*)Ap[b];
+    bt.B[b] = (const unsigned short*)Bp[b];
+    bt.C[b] = C[b];
+  }
+  GNN_REQUIRE(gnn_gemm_p3_packed_bytes(M, K) < (size_t)INT_MAX && gnn_gemm_p3_packed_bytes(N, K) < (size_t)INT_MAX,
+              "gnn_gemm_p3: packed operand >= 2 GiB");
+  hipStream_t st = (hipStream_t)stream;
+  const int Mp = (int)(ceil_div(M, (int64_t)128) * 128), Np = (int)(ceil_div(N, (int64_t)128) * 128);
+  const int KT = (int)ceil_div(K, (int64_t)16);
+  const int splits = K == 0 ? 1 : pick_splits(M, N, K, nbatch, SLOTS_S3);
+  // the split3 kernel's k ranges: ceil(ceil(K / splits) / 16) k tiles per split
+  const int ktlen = splits > 1 ? (int)ceil_div(ceil_div(K, (int64_t)splits), (int64_t)S3_BK) : KT;
+  if (splits > 1) {
+    const size_t need = (size_t)splits * nbatch * M * N * sizeof(float);
+    GNN_REQUIRE(workspace && workspace_bytes >= need, "gnn_gemm_p3: workspace too small (%zu < %zu)", workspace_bytes,
+                need);
+  }
+  int xcdm = 1;
+  if (const char* e = getenv("GNN_GEMM_XCD")) xcdm = atoi(e) != 0;
+  const dim3 grid((unsigned)(Np / BN), (unsigned)(Mp / BM), (unsigned)(nbatch * splits));
+  float* part = (float*)workspace;
+  gemm_p3_kernel<<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, Mp, Np, KT, ldc, splits, ktlen, part, xcdm);
+  GNN_LAUNCHED("gemm_p3_kernel");
+  if (splits > 1) {
+    Batch cb{};
+    for (int b = 0; b < nbatch; ++b) cb.C[b] = C[b];
+    const int64_t total = (int64_t)M * N * nbatch;
+    bool vec4 = ldc == N && (M * N) % 4 == 0;
+    for (int b = 0; b < nbatch; ++b) vec4 = vec4 && (uintptr_t)C[b] % 16 == 0;
+    if (vec4) {
+      const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total / 4, (int64_t)256), 2048);
+      gemm_splitk_reduce4_kernel<<<dim3(g), dim3(256), 0, st>>>(cb, part, M * N, splits, nbatch);
+      GNN_LAUNCHED("gemm_splitk_reduce4_kernel");
+    } else {
+      const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total, (int64_t)256), 2048);
+      gemm_splitk_reduce_kernel<<<dim3(g), dim3(256), 0, st>>>(cb, part, (int)M, (int)N, ldc, splits, nbatch);
+      GNN_LAUNCHED("gemm_splitk_reduce_kernel");
+    }
+  }
+  return 0;
 }
 
 size_t gnn_gemm_f32_split3_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch) {

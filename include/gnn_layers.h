@@ -96,6 +96,20 @@ int gnn_gemm_f32_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N
                                 const float* const* B, int64_t ldb, const int64_t* const* ib, int64_t b_rows,
                                 float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
 
+/* split3 over operands split ONCE into their three bf16 pieces ("p3"): gnn_gemm_p3_pack_f32 writes
+ * an operand viewed as R rows (M for A, N for B) by K — element (r, k) = src[row(r)*ld + k]
+ * (kmajor = 0) or src[row(k)*ld + r] (kmajor = 1), row() through idx when given — as three
+ * zero-padded planes [piece][k tile of 16][R rounded up to 128][16] bf16
+ * (gnn_gemm_p3_packed_bytes(R, K) bytes, 16-byte aligned); gnn_gemm_p3 then computes
+ * C[b] (M x N, row stride ldc) = A[b] · B[b]ᵀ-as-packed with the split3 kernel's tile, k steps
+ * and MFMA order: bit-identical to gnn_gemm_f32_split3 on the same operands. */
+size_t gnn_gemm_p3_packed_bytes(int64_t R, int64_t K);
+int gnn_gemm_p3_pack_f32(const float* src, int64_t ld, int kmajor, const int64_t* idx, int64_t R, int64_t K,
+                         void* out, size_t out_bytes, void* stream);
+size_t gnn_gemm_p3_workspace_bytes(int64_t M, int64_t N, int64_t K, int nbatch);
+int gnn_gemm_p3(int64_t M, int64_t N, int64_t K, int nbatch, const void* const* Ap, const void* const* Bp,
+                float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Classifier head + loss (head.hip). Replaces GNN.forward's tail (models.py:90-97:
  * F.normalize(x, 2, 1) -> dropout(p) -> nn.Linear(D, C)) and utils.loss with sigmoid_loss

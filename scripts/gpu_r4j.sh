@@ -1,4 +1,4 @@
-# Round-4 GPU pass j: spmm / executor tests; the layer-2 forward sweep under rocprofv3; bench A/B of
+# Round-4 GPU pass j: spmm / executor tests; the pre-split (p3) GEMM probe; the layer-2 forward sweep under rocprofv3; bench A/B of
 # the small-operand U = 16 unit kernel (GNN_SPMM_SMALL_U16) and the top layer's small products on
 # the aux stream (GNN_STEP_SMALL_OVERLAP), interleaved; rocprofv3 stats of the default bench.
 set -o pipefail
@@ -9,6 +9,8 @@ REPO=$(pwd)
 timeout -k 10 400 python -u -m pytest tests/test_spmm_gpu.py tests/test_abi.py tests/test_executor_gpu.py \
     tests/test_fused_gpu.py tests/test_configs_gpu.py tests/test_dist_gpu.py -x -q \
     --timeout 200 --timeout-method thread > gpurun_out/gputest_$TAG.log 2>&1 || { echo "tests failed"; exit 1; }
+timeout -k 10 200 python -u scripts/gemm_p3_probe.py --out gpurun_out/gemm_p3_$TAG.json > gpurun_out/gemm_p3_$TAG.log 2>&1 \
+    || { echo "p3 probe failed"; exit 1; }
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_sw_$TAG -o run -- \
     python -u $REPO/scripts/spmm_l2fwd_sweep.py --out $REPO/gpurun_out/l2fwd_sweep_$TAG.json \
     > $REPO/gpurun_out/l2fwd_sweep_$TAG.log 2>&1 || exit 1
