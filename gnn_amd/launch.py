@@ -80,6 +80,12 @@ def launch(argv: List[str], nranks: int, port: Optional[int] = None, poll_s: flo
         raise ValueError(f"nranks must be >= 1, got {nranks}")
     port = port or free_port()
     procs: List[subprocess.Popen] = []
+
+    def on_signal(signum, frame):  # a launcher stopped from outside takes its ranks with it
+        _stop(procs, grace_s)
+        sys.exit(128 + signum)
+
+    old_handlers = {sig: signal.signal(sig, on_signal) for sig in (signal.SIGTERM, signal.SIGHUP)}
     try:
         for r in range(nranks):
             out = None if r == 0 or not quiet_ranks else sys.stderr
@@ -101,6 +107,9 @@ def launch(argv: List[str], nranks: int, port: Optional[int] = None, poll_s: flo
     except BaseException:
         _stop(procs, grace_s)
         raise
+    finally:
+        for sig, h in old_handlers.items():
+            signal.signal(sig, h)
 
 
 def relaunch_self(nranks: int) -> int:

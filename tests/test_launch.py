@@ -97,3 +97,37 @@ def test_bench_relaunches_itself(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert e.value.code == 0 and calls == [2]
+
+
+def test_launcher_stopped_from_outside_stops_its_ranks(tmp_path):
+    """SIGTERM to the launcher (a driver's time limit) ends the ranks too, not just the parent."""
+    import signal
+
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\nopen(sys.argv[1] + '.' + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+                      "time.sleep(600)\n")
+    code = ("import sys; sys.path.insert(0, %r); from gnn_amd import launch; "
+            "sys.exit(launch.launch([sys.executable, %r, %r], 2, grace_s=3.0))" % (REPO, str(script), str(tmp_path / "pid")))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GNN_LAUNCHED_BY")}
+    p = subprocess.Popen([sys.executable, "-c", code], env=env)
+    pids = []
+    for _ in range(200):
+        if all(os.path.exists(tmp_path / f"pid.{r}") for r in range(2)):
+            try:
+                pids = [int((tmp_path / f"pid.{r}").read_text()) for r in range(2)]
+                break
+            except ValueError:
+                pass
+        time.sleep(0.1)
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) == 128 + signal.SIGTERM
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            time.sleep(0.1)
+        else:
+            raise AssertionError(f"rank process {pid} survived its launcher")
