@@ -163,3 +163,46 @@ def test_split3_indexed_rejects_bad_layouts(dev):
     rc = L.gnn_gemm_f32_split3_indexed(1, 0, 64, 64, 64, 1, _ptrs([a]), 64, _ptrs([idx]), 64, _ptrs([a]), 64, None, 0,
                                        _ptrs([c]), 64, None, 0, _lib.stream_of(dev))
     assert rc != 0 and b"row indices" in L.gnn_last_error()
+
+
+@pytest.mark.parametrize("a_km,b_km,M,N,K,nb", [(False, False, 300, 200, 70, 2), (True, True, 130, 257, 4000, 2),
+                                                (False, True, 129, 512, 33, 1), (True, False, 64, 64, 16, 1)])
+def test_p3_packed_equals_split3(dev, a_km, b_km, M, N, K, nb):
+    """gnn_gemm_p3 over operands packed once into their bf16 pieces (gnn_gemm_p3_pack_f32, also
+    through a row index) is bit-identical to gnn_gemm_f32_split3 on the same operands (same pieces,
+    k steps and MFMA order), edge tiles, k tails and split-k included."""
+    import ctypes
+
+    from gnn_amd import _lib
+
+    L = _lib.lib()
+    g = torch.Generator().manual_seed(M + N + K)
+    As = [_operand(a_km, K if a_km else M, M if a_km else K, (M if a_km else K) + 2, g, dev) for _ in range(nb)]
+    Bs = [_operand(b_km, K if b_km else N, N if b_km else K, (N if b_km else K) + 2, g, dev) for _ in range(nb)]
+    ref = gemm(a_km, b_km, As, Bs, M, N, K, algo="split3")
+    st = _lib.stream_of(dev)
+
+    def pack(t, kmajor, R, idx=None):
+        nb_ = L.gnn_gemm_p3_packed_bytes(R, K)
+        out = torch.empty(nb_, dtype=torch.uint8, device=dev)
+        src = t if idx is None else t
+        _lib.check(L.gnn_gemm_p3_pack_f32(src.data_ptr(), src.stride(0), int(kmajor),
+                                          None if idx is None else idx.data_ptr(), R, K, out.data_ptr(), nb_, st),
+                   "gnn_gemm_p3_pack_f32")
+        return out
+
+    pa = [pack(a, a_km, M) for a in As]
+    pb = [pack(b, b_km, N) for b in Bs]
+    C = [torch.full((M, N), float("nan"), device=dev) for _ in range(nb)]
+    wsb = L.gnn_gemm_p3_workspace_bytes(M, N, K, nb)
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    arr = lambda ts: (ctypes.c_void_p * nb)(*[t.data_ptr() for t in ts])
+    _lib.check(L.gnn_gemm_p3(M, N, K, nb, arr(pa), arr(pb), arr(C), N, ws.data_ptr(), wsb, st), "gnn_gemm_p3")
+    torch.cuda.synchronize()
+    for c, r in zip(C, ref):
+        assert torch.equal(c, r)
+    # a row-indexed m-major A (x[sampled]) packs to the same pieces as its gathered copy
+    if not a_km:
+        src = torch.randn(M + 50, As[0].shape[1], device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+        idx = torch.randperm(M + 50, device=dev)[:M]
+        assert torch.equal(pack(src, False, M, idx), pack(src[idx].contiguous(), False, M))
