@@ -445,6 +445,9 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
       else
         grad_row<false, NVH>(src, r, lane, cbase, cend, gx);
     }
+    // the next row's first (col, val) pairs: its range arrived while this row's G rows were awaited,
+    // and the pairs now have the rest of this iteration (reductions, barrier, stores) to arrive
+    if constexpr (AGG) ahead_pairs(src, lane, nx);
 #pragma unroll
     for (int k = 0; k < NVH; ++k) {
       const int c = cbase + (lane + 64 * k) * 4;
@@ -497,7 +500,6 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
         }
       }
     }
-    if constexpr (AGG) ahead_pairs(src, lane, nx);  // the next row's first (col, val) pairs (its range is here)
   }
   // workgroup column sums -> partial[blockIdx.x][q][D]: slot 0 + slot 1 (fixed order)
 #pragma unroll
