@@ -4,7 +4,7 @@ TAG=${1:-r4f}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 REPO=$(pwd)
-timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py tests/test_executor_gpu.py tests/test_fused_gpu.py -x -q \
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q \
     --timeout 300 --timeout-method thread > gpurun_out/gputest_$TAG.log 2>&1 || { echo "tests failed"; exit 1; }
 i=0
 for v in 1 0 1 0; do
