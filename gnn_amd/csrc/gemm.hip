@@ -253,7 +253,18 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce4_kernel(Batch bt, cons
     const int64_t o = (e - (int64_t)b * n4) * 4;
     const float* p = part + (int64_t)b * splits * MN + o;
     f4 acc = *reinterpret_cast<const f4*>(p);
-    for (int q = 1; q < splits; ++q) acc += *reinterpret_cast<const f4*>(p + (int64_t)q * MN);
+    int q = 1;
+    for (; q + 3 < splits; q += 4) {  // 4 partial tiles in flight, added in split order
+      const f4 v0 = *reinterpret_cast<const f4*>(p + (int64_t)q * MN);
+      const f4 v1 = *reinterpret_cast<const f4*>(p + (int64_t)(q + 1) * MN);
+      const f4 v2 = *reinterpret_cast<const f4*>(p + (int64_t)(q + 2) * MN);
+      const f4 v3 = *reinterpret_cast<const f4*>(p + (int64_t)(q + 3) * MN);
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; q < splits; ++q) acc += *reinterpret_cast<const f4*>(p + (int64_t)q * MN);
     *reinterpret_cast<f4*>(bt.C[b] + o) = acc;
   }
 }

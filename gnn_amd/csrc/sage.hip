@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
 
 // Column sums over the G workgroup partials: a workgroup owns FIN_COLS of the NRED*D
 // columns (192 workgroups at D = 1024, not 48: the sum is latency-bound); thread t sums
-// column t % FIN_COLS over the partial rows g = t / FIN_COLS (mod 16), 4 loads in flight,
+// column t % FIN_COLS over the partial rows g = t / FIN_COLS (mod 16), 16 loads in flight,
 // and the 16 group sums are added in a fixed order through LDS (deterministic).
 constexpr int FIN_COLS = 16;
 
@@ -534,6 +534,15 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_finalize_kernel(const float
   if (i < NRED * D) {
     const int64_t stride = (int64_t)NRED * D;
     int g = grp;
+    // 16 loads in flight per thread (the sum is latency-bound: 64 partial rows per thread at
+    // G = 1024), added in row order as they arrive
+    for (; g + 240 < G; g += 256) {
+      float a[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a[k] = partial[(int64_t)(g + 16 * k) * stride + i];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += a[k];
+    }
     for (; g + 48 < G; g += 64) {
       const float a0 = partial[(int64_t)(g + 0) * stride + i];
       const float a1 = partial[(int64_t)(g + 16) * stride + i];
