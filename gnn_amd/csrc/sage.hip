@@ -63,6 +63,40 @@ __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, float p) 
   return (float)(h >> 8) * (1.0f / 16777216.0f) >= p;
 }
 
+// The same mask, computed per row: the inner hash of the element index's high word is the same
+// for every element of a row (or takes two values when the row straddles a multiple of 2^32), so
+// it is hashed twice per row instead of once per element, and the keep test is one integer
+// compare against the threshold T << 8, T = ceil(p * 2^24) (x * 2^-24 >= p <=> x >= T for the
+// integer x = h >> 8 < 2^24; T = 2^24, i.e. p >= 1, keeps nothing). Bit-identical to keep_elem.
+__device__ __forceinline__ uint32_t drop_key(uint64_t seed) {
+  return mix32((uint32_t)seed ^ 0x9e3779b9u) ^ (uint32_t)(seed >> 32);
+}
+
+struct DropThr {
+  uint32_t thr;
+  bool none;
+};
+
+__device__ __forceinline__ DropThr drop_thr(float p) {
+  const float t = ceilf(p * 16777216.0f);
+  if (!(t < 16777216.0f)) return DropThr{0u, true};
+  return DropThr{t <= 0.0f ? 0u : ((uint32_t)t) << 8, false};
+}
+
+struct RowDrop {
+  uint32_t lo0, in0, in1;
+  __device__ __forceinline__ RowDrop(uint32_t key, uint64_t e0) : lo0((uint32_t)e0) {
+    const uint32_t hi0 = (uint32_t)(e0 >> 32);
+    in0 = mix32(hi0 ^ key);
+    in1 = mix32((hi0 + 1u) ^ key);
+  }
+  // keep_elem(seed, e0 + off, p)
+  __device__ __forceinline__ bool keep(uint32_t off, DropThr t) const {
+    const uint32_t lo = lo0 + off;
+    return !t.none && mix32(lo ^ (lo < lo0 ? in1 : in0)) >= t.thr;
+  }
+};
+
 __device__ __forceinline__ float elu1(float h) { return h > 0.0f ? h : expm1f(h); }
 // d elu(h) / dh from the activation o = elu(h): 1 for h > 0 (o > 0), else exp(h) = o + 1
 // (one rounding of expm1(h) + 1 instead of a second exponential).
@@ -265,6 +299,8 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
   }
   const float var = wave_sum(q) / (float)D + 1e-9f;
   const float rstd = rsqrtf(var);
+  const DropThr dt = drop_thr(p);
+  const RowDrop rd(drop_key(seed), (uint64_t)r * (uint64_t)D);
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = (lane + 64 * k) * 4;
@@ -273,11 +309,10 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
       const f4 of = *reinterpret_cast<const f4*>(offset + c);
       f4 y = (o[k] - mean) * sc * rstd + of;
       if (training) {
-        const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
-        y.x = keep_elem(seed, e + 0, p) ? y.x * inv_keep : 0.0f;
-        y.y = keep_elem(seed, e + 1, p) ? y.y * inv_keep : 0.0f;
-        y.z = keep_elem(seed, e + 2, p) ? y.z * inv_keep : 0.0f;
-        y.w = keep_elem(seed, e + 3, p) ? y.w * inv_keep : 0.0f;
+        y.x = rd.keep(c + 0, dt) ? y.x * inv_keep : 0.0f;
+        y.y = rd.keep(c + 1, dt) ? y.y * inv_keep : 0.0f;
+        y.z = rd.keep(c + 2, dt) ? y.z * inv_keep : 0.0f;
+        y.w = rd.keep(c + 3, dt) ? y.w * inv_keep : 0.0f;
       }
       *reinterpret_cast<f4*>(Y + (int64_t)r * ldy + c) = y;
     }
@@ -305,9 +340,12 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
     db[k] = f4(0.0f);
     dbi[k] = f4(0.0f);
   }
+  const DropThr dt = drop_thr(p);
+  const uint32_t dkey = drop_key(seed);
   for (int r = blockIdx.x * 4 + w; r < M; r += gridDim.x * 4) {
     const float m = mean[r];
     const float rs = rstd[r];
+    const RowDrop rd(dkey, (uint64_t)r * (uint64_t)D);
     f4 h[NV], xh[NV], gx[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {  // pre-activations first (overlapping the gradient's chain)
@@ -327,11 +365,10 @@ __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
         xh[k] = (o - m) * rs;
         f4 g = gx[k];
         if (training) {
-          const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
-          g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
-          g.y = keep_elem(seed, e + 1, p) ? g.y * inv_keep : 0.0f;
-          g.z = keep_elem(seed, e + 2, p) ? g.z * inv_keep : 0.0f;
-          g.w = keep_elem(seed, e + 3, p) ? g.w * inv_keep : 0.0f;
+          g.x = rd.keep(c + 0, dt) ? g.x * inv_keep : 0.0f;
+          g.y = rd.keep(c + 1, dt) ? g.y * inv_keep : 0.0f;
+          g.z = rd.keep(c + 2, dt) ? g.z * inv_keep : 0.0f;
+          g.w = rd.keep(c + 3, dt) ? g.w * inv_keep : 0.0f;
         }
         db[k] += g;
         ds[k] += g * xh[k];
@@ -391,8 +428,9 @@ int bwd2_grid_cap(bool agg) {
   return v > 0 && v <= BWD2_GRID_SWEEP_MAX ? v : BWD2_MAX_GRID;
 }
 
+// 4 workgroups per CU at D <= 1024 (<= 128 VGPRs with the next row's loads held)
 template <int NVH, bool AGG>
-__global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NVH <= 2 ? 4 : 1))) void sage_norm_bwd2_kernel(
     GradSrc src, const float* __restrict__ hB, int64_t ldb,
     const float* __restrict__ bB, int D1, const float* __restrict__ hW, int64_t ldw, const float* __restrict__ bW,
     int D, const float* __restrict__ scale, const float* __restrict__ mean, const float* __restrict__ rstd, int M,
@@ -413,66 +451,79 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
     db[k] = f4(0.0f);
     dbi[k] = f4(0.0f);
   }
+  const DropThr dt = drop_thr(p);
+  const uint32_t dkey = drop_key(seed);
   int it = 0;
   Ahead nx{};  // AGG: the chain of this wave's next row, loaded one iteration ahead
   if constexpr (AGG) {
     ahead_range(src, blockIdx.x * 2 + slot, M, lane, nx);
     ahead_pairs(src, lane, nx);
   }
-  for (int r0 = blockIdx.x * 2; r0 < M; r0 += gridDim.x * 2, ++it) {
-    const int r = r0 + slot;
-    const bool live = r < M;
-    f4 eg[NVH], xh[NVH], gx[NVH];
-    float a = 0.0f, b = 0.0f;
-    float m = 0.0f, rs = 0.0f;
-    f4 hv[NVH];
-    Ahead cur{};
-    if constexpr (AGG) cur = nx;
-    if (live) {
-      m = mean[r];
-      rs = rstd[r];
-      // the row's pre-activations first: their loads overlap the gradient's G-row loads
+  // The next row's pre-activations, saved statistics and (dense form) output gradient are loaded
+  // one iteration ahead: they arrive while this row is reduced, exchanged and stored (the kernel
+  // is latency-bound at 4 workgroups per CU; loads stay in flight across the LDS barrier).
+  const int rstride = gridDim.x * 2;
+  f4 hn[NVH], gn[NVH];
+  float mn = 0.0f, rsn = 0.0f;
+  auto load_next = [&](int rr) {
+    if (rr < M) {
+      mn = mean[rr];
+      rsn = rstd[rr];
 #pragma unroll
       for (int k = 0; k < NVH; ++k) {
         const int c = cbase + (lane + 64 * k) * 4;
-        hv[k] = c < cend ? load_h(hB, ldb, bB, D1, hW, ldw, bW, r, c) : f4(0.0f);
+        hn[k] = c < cend ? load_h(hB, ldb, bB, D1, hW, ldw, bW, rr, c) : f4(0.0f);
       }
+      if constexpr (!AGG) grad_row<false, NVH>(src, rr, lane, cbase, cend, gn);
     }
-    if constexpr (AGG) ahead_range(src, r + gridDim.x * 2, M, lane, nx);  // the next row's range
-    if (live) {
-      if constexpr (AGG)
-        grad_row_ahead<NVH>(src, cur, lane, cbase, cend, gx);  // the output gradient, scaled below
-      else
-        grad_row<false, NVH>(src, r, lane, cbase, cend, gx);
+  };
+  load_next(blockIdx.x * 2 + slot);
+  for (int r0 = blockIdx.x * 2; r0 < M; r0 += rstride, ++it) {
+    const int r = r0 + slot;
+    const bool live = r < M;
+    f4 gx[NVH];
+    float a = 0.0f, b = 0.0f;
+    const float m = mn, rs = rsn;
+    f4 hv[NVH];
+#pragma unroll
+    for (int k = 0; k < NVH; ++k) {
+      hv[k] = hn[k];
+      if constexpr (!AGG) gx[k] = gn[k];
+    }
+    Ahead cur{};
+    if constexpr (AGG) cur = nx;
+    load_next(r + rstride);
+    if constexpr (AGG) {
+      ahead_range(src, r + rstride, M, lane, nx);  // the next row's range
+      if (live) grad_row_ahead<NVH>(src, cur, lane, cbase, cend, gx);  // the output gradient, scaled below
     }
     // the next row's first (col, val) pairs: its range arrived while this row's G rows were awaited,
     // and the pairs now have the rest of this iteration (reductions, barrier, stores) to arrive
     if constexpr (AGG) ahead_pairs(src, lane, nx);
+    const RowDrop rd(dkey, (uint64_t)r * (uint64_t)D);
 #pragma unroll
     for (int k = 0; k < NVH; ++k) {
       const int c = cbase + (lane + 64 * k) * 4;
       if (live && c < cend) {
         const f4 hk = hv[k];
         const f4 o = f4{elu1(hk.x), elu1(hk.y), elu1(hk.z), elu1(hk.w)};
-        eg[k] = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
-                   elu1_grad_from_out(o.w)};
-        xh[k] = (o - m) * rs;
+        hv[k] = o;  // the activation: xh and the ELU derivative are recomputed from it below
+        const f4 xh = (o - m) * rs;
         f4 g = gx[k];
         if (training) {
-          const uint64_t e = (uint64_t)r * (uint64_t)D + (uint64_t)c;
-          g.x = keep_elem(seed, e + 0, p) ? g.x * inv_keep : 0.0f;
-          g.y = keep_elem(seed, e + 1, p) ? g.y * inv_keep : 0.0f;
-          g.z = keep_elem(seed, e + 2, p) ? g.z * inv_keep : 0.0f;
-          g.w = keep_elem(seed, e + 3, p) ? g.w * inv_keep : 0.0f;
+          g.x = rd.keep(c + 0, dt) ? g.x * inv_keep : 0.0f;
+          g.y = rd.keep(c + 1, dt) ? g.y * inv_keep : 0.0f;
+          g.z = rd.keep(c + 2, dt) ? g.z * inv_keep : 0.0f;
+          g.w = rd.keep(c + 3, dt) ? g.w * inv_keep : 0.0f;
         }
         db[k] += g;
-        ds[k] += g * xh[k];
+        ds[k] += g * xh;
         gx[k] = g * *reinterpret_cast<const f4*>(scale + c);
-        const f4 gxx = gx[k] * xh[k];
+        const f4 gxx = gx[k] * xh;
         a += (gx[k].x + gx[k].y) + (gx[k].z + gx[k].w);
         b += (gxx.x + gxx.y) + (gxx.z + gxx.w);
       } else {
-        eg[k] = xh[k] = gx[k] = f4(0.0f);
+        hv[k] = gx[k] = f4(0.0f);
       }
     }
     a = wave_sum(a);
@@ -490,7 +541,11 @@ __global__ __launch_bounds__(256) void sage_norm_bwd2_kernel(
       for (int k = 0; k < NVH; ++k) {
         const int c = cbase + (lane + 64 * k) * 4;
         if (c < cend) {
-          const f4 dh = rs * (gx[k] - A - xh[k] * B) * eg[k];
+          const f4 o = hv[k];
+          const f4 xh = (o - m) * rs;
+          const f4 eg = f4{elu1_grad_from_out(o.x), elu1_grad_from_out(o.y), elu1_grad_from_out(o.z),
+                           elu1_grad_from_out(o.w)};
+          const f4 dh = rs * (gx[k] - A - xh * B) * eg;
           dbi[k] += dh;
           if (c < D1) {
             *reinterpret_cast<f4*>(dhB + (int64_t)r * D1 + c) = dh;

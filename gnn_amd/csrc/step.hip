@@ -505,28 +505,29 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
   // ------------------------------------------------------------------ backward
   GNN_TRY(gnn_head_bce_bwd_f32(top.Y, top.D, pl.Mh, pl.Dh, Wh, pl.C, labels, ldl, nullptr, p, hseed, training, pl.z,
                                pl.nrm, pl.dz, pl.dXh, pl.Dh, st));
-  // the head's weight and bias gradients: on the aux stream beside the top layer's backward
-  hipStream_t shead = st;
-  rocblas_handle hhead = h;
-  if (ha) {
-    GNN_TRY(fork_join(aux, st, aux->s));
-    shead = aux->s;
-    hhead = ha;
-    aux_used = true;
-  }
-  GNN_TRY(mm_gtx(hhead, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
-  if (HP<float>(d, GNN_SH_HEAD_GB)) {
-    colsum_kernel<<<dim3((unsigned)pl.C), dim3(256), 0, shead>>>(pl.dz, (int)pl.Mh, (int)pl.C,
-                                                               HP<float>(d, GNN_SH_HEAD_GB));
-    GNN_LAUNCHED("colsum_kernel");
-  }
   // gradient-ready events (GNN_SH_GRAD_EVENTS): the caller's DP exchange of a bucket starts there
   const int64_t* const E = HP<const int64_t>(d, GNN_SH_GRAD_EVENTS);
   auto grads_ready = [&](int64_t slot, hipStream_t s) -> int {
     if (E && slot < E[0] && E[slot]) GNN_HIP(hipEventRecord((hipEvent_t)E[slot], s), "hipEventRecord (grad event)");
     return 0;
   };
-  GNN_TRY(grads_ready(1, shead));
+  // the head's weight and bias gradients (their inputs are final here). With the aux stream they
+  // go there with the first small weight-gradient products of the backward below, behind the same
+  // fork: every event recorded on or awaited by the step's stream costs it a ~7 us bubble between
+  // kernels (profiles/round4/trace/), so the backward forks once, not twice.
+  bool head_pending = true;
+  auto head_grads = [&](hipStream_t s, rocblas_handle hh) -> int {
+    GNN_TRY(mm_gtx(hh, pl.dz, pl.C, pl.xd, pl.Dh, HP<float>(d, GNN_SH_HEAD_GW), pl.Dh, pl.C, pl.Dh, pl.Mh));
+    if (HP<float>(d, GNN_SH_HEAD_GB)) {
+      colsum_kernel<<<dim3((unsigned)pl.C), dim3(256), 0, s>>>(pl.dz, (int)pl.Mh, (int)pl.C,
+                                                             HP<float>(d, GNN_SH_HEAD_GB));
+      GNN_LAUNCHED("colsum_kernel");
+    }
+    GNN_TRY(grads_ready(1, s));
+    head_pending = false;
+    return 0;
+  };
+  if (!ha) GNN_TRY(head_grads(st, h));
   for (int l = pl.nl - 1; l >= 0; --l) {
     LayerBufs& b = pl.lb[l];
     const int64_t N = b.N;
@@ -594,6 +595,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
         sw = aux->s;
         hw = ha;
         aux_used = true;
+        if (head_pending) GNN_TRY(head_grads(aux->s, ha));
       }
       if (pl.sage) GNN_TRY(mm_gtx(hw, b.dhB, N, b.xs, b.ldo, gWB, b.F, N, b.F, b.M));
       GNN_TRY(mm_gtx(hw, b.dhW, N, b.feat, b.ldo, gWW, b.F, N, b.F, b.M));
@@ -628,6 +630,11 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
                                  b.ws_bwd, b.b_bwd, 0, st));
       }
     }
+  }
+  if (head_pending) {  // no small weight-gradient fork above: the head's own
+    GNN_TRY(fork_join(aux, st, aux->s));
+    GNN_TRY(head_grads(aux->s, ha));
+    aux_used = true;
   }
   if (aux_used) GNN_TRY(fork_join(aux, aux->s, st));
   return 0;
