@@ -454,7 +454,8 @@ __device__ __forceinline__ void s3_mma(const unsigned short* __restrict__ Sa, co
 template <bool AK, bool BKM, int VA, int VB, bool IDX = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void gemm_s3_kernel(Batch bt, int M, int N, int K, int64_t lda, int64_t ldb,
                                                          int64_t ldc, int splits, int klen, float* __restrict__ part,
-                                                         int64_t abytes, int64_t bbytes, int xcd_map) {
+                                                         int64_t abytes, int64_t bbytes, int xcd_map,
+                                                         int tail_base = 0, int tail_s = 0) {
   __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
   __shared__ __attribute__((aligned(16))) unsigned short Bs[2][S3_OPER];
   const int t = threadIdx.x;
@@ -465,22 +466,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   // go to one XCD (workgroups are dealt to the 8 XCDs round-robin), so a row panel of A is
   // fetched into one L2 instead of up to four.
   int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
-  if (xcd_map) {
-    const int gx = gridDim.x, gy = gridDim.y;
-    const int total = gx * gy * gridDim.z;
-    const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-    const int per = total >> 3;
-    const int lg = hw < per * 8 ? (hw & 7) * per + (hw >> 3) : hw;
+  int b, split;
+  int piece = -1;  // tail mode: this workgroup's k piece of a tail tile (slot in the piece slab)
+  if (tail_s > 0) {
+    // 1-D grid: tiles [0, tail_base) whole (XCD map over them), then each tail tile as tail_s
+    // k pieces (see tail_plan)
+    const int gx = (N + BN - 1) / BN, gy = (M + BM - 1) / BM;
+    const int hw = blockIdx.x;
+    int lg;
+    if (hw < tail_base) {
+      const int per = tail_base >> 3;
+      lg = xcd_map ? (hw & 7) * per + (hw >> 3) : hw;
+      split = 0;
+    } else {
+      piece = hw - tail_base;
+      lg = tail_base + piece / tail_s;
+      split = piece % tail_s;
+    }
     tx = lg % gx;
     ty = (lg / gx) % gy;
-    tz = lg / (gx * gy);
+    b = lg / (gx * gy);
+  } else {
+    if (xcd_map) {
+      const int gx = gridDim.x, gy = gridDim.y;
+      const int total = gx * gy * gridDim.z;
+      const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+      const int per = total >> 3;
+      const int lg = hw < per * 8 ? (hw & 7) * per + (hw >> 3) : hw;
+      tx = lg % gx;
+      ty = (lg / gx) % gy;
+      tz = lg / (gx * gy);
+    }
+    b = tz / splits;
+    split = tz % splits;
   }
-  const int b = tz / splits;
-  const int split = tz % splits;
   const int m0 = ty * BM;
   const int n0 = tx * BN;
-  const int kbeg = split * klen;
-  const int kend = min(K, kbeg + klen);
+  const bool whole = tail_s > 0 && piece < 0;
+  const int kbeg = whole ? 0 : split * klen;
+  const int kend = whole ? K : min(K, kbeg + klen);
   const float* __restrict__ A = bt.A[b];
   const float* __restrict__ B = bt.B[b];
   const __amdgpu_buffer_rsrc_t rsa = s3_rsrc(A, abytes), rsb = s3_rsrc(B, bbytes);
@@ -554,6 +578,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     s3_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 64, li, lh, acc);
   }
 
+  if (piece >= 0) {  // a tail tile's k piece: the whole 128 x 128 tile, tile-local, into its slab slot
+    float* __restrict__ P = part + (int64_t)piece * (BM * BN);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          P[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * BN + wn * 64 + j * 32 + li] = acc[i][j][r];
+    return;
+  }
   float* __restrict__ Cb;
   int64_t ldo;
   if (splits > 1) {
@@ -579,6 +614,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 }
 
 // ---------------------------------------------------------------------------------
+
+// The tail tiles' k pieces summed in piece order into C: 16 workgroups per tile, a float4 of the
+// tile per thread.
+__global__ __launch_bounds__(256) void gemm_tail_reduce_kernel(Batch bt, const float* __restrict__ part, int M, int N,
+                                                               int64_t ldc, int tail_base, int tail_s) {
+  const int tile = blockIdx.x >> 4;
+  const int e4 = (blockIdx.x & 15) * 256 + threadIdx.x;  // float4 of the tile, 0 .. 4095
+  const int ml = e4 >> 5, nl = (e4 & 31) * 4;
+  const float* p = part + (int64_t)tile * tail_s * (BM * BN) + ml * BN + nl;
+  f4 acc = *reinterpret_cast<const f4*>(p);
+  for (int q = 1; q < tail_s; ++q) acc += *reinterpret_cast<const f4*>(p + (int64_t)q * (BM * BN));
+  const int gx = (N + BN - 1) / BN, gy = (M + BM - 1) / BM;
+  const int lg = tail_base + tile;
+  const int m = ((lg / gx) % gy) * BM + ml, n = (lg % gx) * BN + nl;
+  if (m >= M) return;
+  float* c = bt.C[lg / (gx * gy)] + (int64_t)m * ldc + n;
+  if (n + 0 < N) c[0] = acc.x;
+  if (n + 1 < N) c[1] = acc.y;
+  if (n + 2 < N) c[2] = acc.z;
+  if (n + 3 < N) c[3] = acc.w;
+}
+
 // "p3": split3 on operands split ONCE into their three bf16 pieces in HBM (gnn_gemm_p3_pack_f32)
 // instead of in every workgroup's registers. The split3 kernel spends ~3 of its ~5 vector
 // instructions per MFMA on the split (and/sub/perm), and it is bound by the SIMD's issue port
@@ -771,6 +828,41 @@ int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch, int64_t slots) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
+// Tail tiles (split3, unsplit k): a launch of T tiles over 256 CUs whose last partial round holds
+// only rem = T mod 256 tiles (the layer-1 forward's 544 = 2 x 256 + 32) pays for that round almost
+// like a full one (scripts/gemm_tiles_probe.py: 512 tiles 104 us, 544 126 us, 768 139 us). The
+// first T - rem tiles run whole and each tail tile is cut into S = 4 k pieces (>= 4 k tiles each),
+// small pieces beside the whole tiles of 4 rem CUs; gemm_tail_reduce_kernel adds a tail tile's
+// pieces in order (deterministic; those tiles are summed in S chains instead of one). rem <= 32
+// only: at the layer-1 input gradient's 64 (1,088 tiles) the pieces + their reduction cost more
+// than the round they save (profiles/round4/gemm_tail/); GNN_GEMM_TAIL=0 turns it off (A/B).
+struct TailPlan {
+  int base = 0;  // whole tiles
+  int s = 0;     // pieces per tail tile (0: off)
+  int rem = 0;
+};
+
+TailPlan tail_plan(int64_t M, int64_t N, int64_t K, int nbatch) {
+  TailPlan tp;
+  const int64_t T = ceil_div(M, (int64_t)BM) * ceil_div(N, (int64_t)BN) * nbatch;
+  if (T <= 256 || T >= INT_MAX / 2) return tp;
+  const int64_t rem = T % 256;
+  if (rem == 0 || rem > 32) return tp;
+  const int64_t S = std::min<int64_t>(std::min<int64_t>(256 / rem, 4), ceil_div(K, (int64_t)16) / 4);
+  if (S < 2) return tp;
+  tp.base = (int)(T - rem);
+  tp.s = (int)S;
+  tp.rem = (int)rem;
+  return tp;
+}
+
+bool tail_enabled() {
+  const char* e = getenv("GNN_GEMM_TAIL");  // per call (tests toggle it)
+  return !(e && atoi(e) == 0);
+}
+
+size_t tail_bytes(const TailPlan& tp) { return (size_t)tp.rem * tp.s * BM * BN * sizeof(float); }
+
 enum Algo { ALGO_F32 = 0, ALGO_S3 = 1 };
 
 int64_t slots_of(int algo) { return algo == ALGO_S3 ? SLOTS_S3 : SLOTS_F32; }
@@ -832,23 +924,29 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
   int bkt = algo == ALGO_S3 ? S3_BK : 32;
   if (algo == ALGO_F32)
     if (const char* e = getenv("GNN_GEMM_BKT")) bkt = atoi(e) == 16 ? 16 : 32;  // experiments
-  const int klen = splits > 1 ? (int)(ceil_div(ceil_div(K, (int64_t)splits), (int64_t)bkt) * bkt) : (int)K;
-  if (splits > 1) {
-    const size_t need = (size_t)splits * nbatch * M * N * sizeof(float);
+  TailPlan tp;
+  if (algo == ALGO_S3 && splits == 1 && split_nbatch == 0 && K > 0 && tail_enabled()) tp = tail_plan(M, N, K, nbatch);
+  int klen = splits > 1 ? (int)(ceil_div(ceil_div(K, (int64_t)splits), (int64_t)bkt) * bkt) : (int)K;
+  if (tp.s > 0) klen = (int)(ceil_div(ceil_div(K, (int64_t)tp.s), (int64_t)bkt) * bkt);
+  if (splits > 1 || tp.s > 0) {
+    const size_t need = splits > 1 ? (size_t)splits * nbatch * M * N * sizeof(float) : tail_bytes(tp);
     GNN_REQUIRE(workspace && workspace_bytes >= need, "gnn_gemm_f32: workspace too small (%zu < %zu)",
                 workspace_bytes, need);
   }
-  const dim3 grid((unsigned)ceil_div(N, (int64_t)BN), (unsigned)ceil_div(M, (int64_t)BM), (unsigned)(nbatch * splits));
+  const dim3 grid = tp.s > 0 ? dim3((unsigned)(tp.base + tp.rem * tp.s))
+                             : dim3((unsigned)ceil_div(N, (int64_t)BN), (unsigned)ceil_div(M, (int64_t)BM),
+                                    (unsigned)(nbatch * splits));
   float* part = (float*)workspace;
 #define GNN_GEMM_LAUNCH(AK, BK, VA, VB)                                                                     \
   do {                                                                                                        \
     if (algo == ALGO_S3 && idx)                                                                               \
       gemm_s3_kernel<AK, BK, VA, VB, true><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb,  \
                                                                        ldc, splits, klen, part, abytes, bbytes, \
-                                                                       xcdm);                                   \
+                                                                       xcdm, tp.base, tp.s);                    \
     else if (algo == ALGO_S3)                                                                                 \
       gemm_s3_kernel<AK, BK, VA, VB><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc,  \
-                                                                 splits, klen, part, abytes, bbytes, xcdm);   \
+                                                                 splits, klen, part, abytes, bbytes, xcdm,    \
+                                                                 tp.base, tp.s);                              \
     else if (bkt == 16)                                                                                       \
       gemm_f32_kernel<AK, BK, VA, VB, 16>                                                                     \
           <<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc, splits, klen, part);        \
@@ -870,6 +968,11 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 #undef GNN_GEMM_V
 #undef GNN_GEMM_LAUNCH
   GNN_LAUNCHED(algo == ALGO_S3 ? "gemm_s3_kernel" : "gemm_f32_kernel");
+  if (tp.s > 0) {
+    gemm_tail_reduce_kernel<<<dim3((unsigned)(tp.rem * 16)), dim3(256), 0, st>>>(bt, part, (int)M, (int)N, ldc,
+                                                                                tp.base, tp.s);
+    GNN_LAUNCHED("gemm_tail_reduce_kernel");
+  }
   if (splits > 1) {
     const int64_t total = (int64_t)M * N * nbatch;
     bool vec4 = ldc == N && (M * N) % 4 == 0;
@@ -890,7 +993,8 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 size_t workspace_bytes_of(int algo, int64_t M, int64_t N, int64_t K, int nbatch) {
   if (M <= 0 || N <= 0 || K <= 0 || nbatch <= 0) return 0;
   const int s = pick_splits(M, N, K, nbatch, slots_of(algo));
-  return s > 1 ? (size_t)s * nbatch * M * N * sizeof(float) : 0;
+  if (s > 1) return (size_t)s * nbatch * M * N * sizeof(float);
+  return algo == ALGO_S3 ? tail_bytes(tail_plan(M, N, K, nbatch)) : 0;  // whatever GNN_GEMM_TAIL says
 }
 
 }  // namespace

@@ -206,3 +206,24 @@ def test_p3_packed_equals_split3(dev, a_km, b_km, M, N, K, nb):
         src = torch.randn(M + 50, As[0].shape[1], device=dev, generator=torch.Generator(device=dev).manual_seed(5))
         idx = torch.randperm(M + 50, device=dev)[:M]
         assert torch.equal(pack(src, False, M, idx), pack(src[idx].contiguous(), False, M))
+
+
+def test_split3_tail_tiles(dev, monkeypatch):
+    """Tail tiles (gemm.hip tail_plan) on the layer-1 forward shape: 544 tiles = 2 x 256 whole + 32
+    tail tiles computed as 4 k pieces each and added in piece order. Against fp64 within the module
+    tolerance; the whole tiles bit-identical to the unsplit launch (GNN_GEMM_TAIL=0), the tail tiles
+    (batch 1, rows >= 7,680) within fp32 rounding of it; deterministic."""
+    M, N, K = 8680, 512, 1024
+    _check(False, False, M, N, K, 2, dev, algo="split3")
+    g = torch.Generator().manual_seed(5)
+    As = [_operand(False, M, K, K, g, dev) for _ in range(2)]
+    Bs = [_operand(False, N, K, K, g, dev) for _ in range(2)]
+    on = gemm(False, False, As, Bs, M, N, K, algo="split3")
+    again = gemm(False, False, As, Bs, M, N, K, algo="split3")
+    monkeypatch.setenv("GNN_GEMM_TAIL", "0")
+    off = gemm(False, False, As, Bs, M, N, K, algo="split3")
+    torch.cuda.synchronize()
+    assert all(torch.equal(x, y) for x, y in zip(on, again))
+    assert torch.equal(on[0], off[0]) and torch.equal(on[1][:7680], off[1][:7680])
+    d = (on[1][7680:] - off[1][7680:]).abs().max().item()
+    assert 0 < d <= 1e-4 * off[1][7680:].abs().max().item()
