@@ -652,52 +652,77 @@ def _main(args, held):
     lo_pri, hi_pri = torch.cuda.Stream.priority_range()
     compute_stream = torch.cuda.Stream(device=dev, priority=hi_pri) if args.compute_priority == "high" else None
 
-    def pipeline(next_item, steps):
+    def pipeline(next_item, steps, carry=None):
         if compute_stream is None:
-            return _pipeline(next_item, steps)
+            return _pipeline(next_item, steps, carry)
         compute_stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(compute_stream):
-            loss = _pipeline(next_item, steps)
+            loss = _pipeline(next_item, steps, carry)
         torch.cuda.current_stream(dev).wait_stream(compute_stream)
         return loss
 
-    def _pipeline(next_item, steps):
+    def _pipeline(next_item, steps, carry=None):
         """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
         needed + the operand builds). The X0 staging and batch_fn of batches i+1 .. i+A (A =
         --stage-ahead) run on the side stream, issued before batch i's step, so they overlap
         that step's kernels; with A = 2 a batch's staging has two steps' worth of the compute
         stream's gaps to finish in (the compute kernels fill every CU, so staging kernels run
-        only in their gaps), and the compute stream does not wait for it between steps."""
+        only in their gaps), and the compute stream does not wait for it between steps.
+        `carry` (a deque kept by the caller): the live stream's A staged-ahead batches persist
+        from one call to the next, so a timed pass starts in the steady state the warm-up left
+        (its first step's X0 already staged) and issues one staging per step like every other
+        step, instead of refilling the pipeline inside the timed region (20-step windows read
+        520-592 mini-batches/s that way against 600 over 300 steps)."""
         loss = None
-        ahead = collections.deque()
+        persistent = carry is not None
+        ahead = carry if persistent else collections.deque()
         issued = 0
-        while issued < min(args.stage_ahead, steps):
+        if persistent:
+            # one more in flight than --stage-ahead: the next staging is issued after the step
+            # below, so batch i + A + 1's staging gets step i + 1's duration, as batch i + A's got
+            # step i's when it was issued before the step
+            while len(ahead) < max(1, args.stage_ahead) + 1:
+                ahead.append(stager.issue(*next_item()))
+        while not persistent and issued < min(args.stage_ahead, steps):
             ahead.append(stager.issue(*next_item()))
             issued += 1
         for i in range(steps):
             staged = ahead.popleft()
-            if issued < steps:
+            if not persistent and issued < steps:
                 ahead.append(stager.issue(*next_item()))
                 issued += 1
             x0 = staged.wait(retire)
             db = staged.batch
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
+            if persistent:
+                # the next batch's staging after this step's launches (its own stream: it still
+                # overlaps this step), so a timed pass's first kernels start without waiting for it
+                ahead.append(stager.issue(*next_item()))
         return loss
 
     def timed(fn_):
-        """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds)."""
+        """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds).
+        Python's cyclic GC is collected before and paused inside the timed region (a gen-2 pass
+        over the process's objects would land in a 33 ms window as a multi-ms stall)."""
+        import gc
+
+        gc.collect()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         retire.wait_s = 0.0
-        ts = time.perf_counter()
-        out = fn_()
-        issued = time.perf_counter() - ts - retire.wait_s
-        torch.cuda.synchronize()
-        if world > 1:
-            torch.distributed.barrier()
-        el = time.perf_counter() - ts
+        gc.disable()
+        try:
+            ts = time.perf_counter()
+            out = fn_()
+            issued = time.perf_counter() - ts - retire.wait_s
+            torch.cuda.synchronize()
+            if world > 1:
+                torch.distributed.barrier()
+            el = time.perf_counter() - ts
+        finally:
+            gc.enable()
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -737,8 +762,12 @@ def _main(args, held):
     # warm-up: at least the prefetch queue's depth, so the timed steps start in steady state
     # (the queue filled during setup holds pre-sampled batches that must not be timed)
     warm = max(args.warmup, loader.prefetch + 2)
-    pipeline(nxt_live, warm)
-    e2e_s, e2e_issue, loss = timed(lambda: pipeline(nxt_live, args.steps))
+    live_ahead = collections.deque()
+    pipeline(nxt_live, warm, live_ahead)
+    e2e_s, e2e_issue, loss = timed(lambda: pipeline(nxt_live, args.steps, live_ahead))
+    # the batches staged for steps past the window: let their staging finish, then drop them
+    torch.cuda.synchronize()
+    live_ahead.clear()
     log(f"end to end: {world * args.steps / e2e_s:.1f} mini-batches/s ({time.time() - t0:.1f}s)")
 
     # ------------------------------------------------- GPU step over distinct pre-sampled batches
