@@ -19,7 +19,7 @@ def main():
         r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     rows.sort(key=lambda r: r["s"])
     ad = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
-    i0, i1 = ad[-k - 1], ad[-k]
+    i0, i1 = ad[-k - 1], ad[-k]  # k > 0: from the end; k < 0: from the start
     t0 = rows[i0]["e"]
     cq = rows[i1]["Queue_Id"]
     last_end, gaps = t0, 0.0
