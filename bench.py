@@ -108,6 +108,9 @@ def parse():
                          "per batch after a host negotiation; every N > 1 run also times the other form")
     ap.add_argument("--stage-ahead", type=int, default=int(os.environ.get("GNN_STAGE_AHEAD", "1")),
                     help="batches whose X0 staging / device side are issued ahead of the current step")
+    ap.add_argument("--stage-gate", type=int, default=int(os.environ.get("GNN_STAGE_GATE", "1")),
+                    help="the next batches' X0 gathers and layer extractions wait for this layer's forward "
+                         "aggregation of the current step (an event the executor records; -1: no gate)")
     ap.add_argument("--numa", default="off", choices=["gpu", "off"],
                     help="confine the process (training + producer threads) to the CPUs of the GPU's NUMA node "
                          "(A/B on one box, 3 runs each: 572 vs 584 mini-batches/s unpinned, so off by default)")
@@ -642,6 +645,10 @@ def _main(args, held):
     torch.manual_seed(0)
     model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
     trainer = Trainer(model, args.lr, dev)
+    if args.stage_gate >= 0:
+        gate = torch.cuda.Event()
+        trainer.stage_gate = (gate, args.stage_gate)
+        stager.gate = gate
     torch.cuda.synchronize()
     log(f"setup done ({time.time() - t0:.1f}s); params={trainer.num_params}")
     retire = staging.Retirement()
@@ -683,22 +690,23 @@ def _main(args, held):
             # step i's when it was issued before the step
             while len(ahead) < max(1, args.stage_ahead) + 1:
                 ahead.append(stager.issue(*next_item()))
-        while not persistent and issued < min(args.stage_ahead, steps):
+        while not persistent and issued < min(max(1, args.stage_ahead) + 1, steps):
             ahead.append(stager.issue(*next_item()))
             issued += 1
         for i in range(steps):
             staged = ahead.popleft()
-            if not persistent and issued < steps:
-                ahead.append(stager.issue(*next_item()))
-                issued += 1
             x0 = staged.wait(retire)
             db = staged.batch
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
+            # the next batch's staging after this step's launches (its own stream: it still
+            # overlaps this step, behind --stage-gate's event when set), so a timed pass's first
+            # kernels start without waiting for it
             if persistent:
-                # the next batch's staging after this step's launches (its own stream: it still
-                # overlaps this step), so a timed pass's first kernels start without waiting for it
                 ahead.append(stager.issue(*next_item()))
+            elif issued < steps:
+                ahead.append(stager.issue(*next_item()))
+                issued += 1
         return loss
 
     def timed(fn_):
@@ -992,7 +1000,7 @@ def _main(args, held):
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "peer_rows": (args.peer_rows if world > 1 else None),
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
-                       "stage_ahead": args.stage_ahead,
+                       "stage_ahead": args.stage_ahead, "stage_gate": args.stage_gate,
                        "locality_sampling": args.locality_sampling, "scale_factor": args.scale_factor,
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",

@@ -412,6 +412,13 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
     const int64_t v[] = {kind, l, M, K, nnz, F, Fk, ldx, ldo, (int64_t)(uintptr_t)X, (int64_t)(uintptr_t)Y, res_rows, 1};
     std::memcpy(r + 2, v, sizeof v);
   };
+  // the staging gate (GNN_SH_STAGE_EVENT): recorded right after the chosen layer's forward
+  // aggregation is issued
+  auto stage_gate = [&](int l) -> int {
+    if (d[GNN_SH_STAGE_EVENT] && l == (int)d[GNN_SH_STAGE_LAYER])
+      GNN_HIP(hipEventRecord((hipEvent_t)d[GNN_SH_STAGE_EVENT], st), "hipEventRecord (stage gate)");
+    return 0;
+  };
   // ------------------------------------------------------------------ forward
   for (int l = 0; l < pl.nl; ++l) {
     LayerBufs& b = pl.lb[l];
@@ -440,6 +447,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
                                P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
                                b.ws_fwd, b.b_fwd, 0, st));
+      GNN_TRY(stage_gate(l));
       const float* Aw[1] = {b.feat};
       const float* Bw[1] = {WW};
       float* Cw[1] = {b.hW};
@@ -455,6 +463,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
                                P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
                                b.ws_fwd, b.b_fwd, 0, st));
+      GNN_TRY(stage_gate(l));
       GNN_TRY(mm_xwt(h, b.feat, b.ldo, WW, b.F, b.hW, N, b.M, N, b.F));
       GNN_TRY(fork_join(aux, aux->s, st));  // the tail reads hB
     } else {
@@ -462,6 +471,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
                                P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
                                b.ws_fwd, b.b_fwd, 0, st));
+      GNN_TRY(stage_gate(l));
       // x[sampled] feeds only linearB and its weight gradient: when both run on split3 (and X's
       // rows have the aggregation output's stride) the GEMMs read X's rows through the index
       // instead of a gathered copy (bit-identical operands)

@@ -24,7 +24,8 @@ from . import custom_sparse_ops as cso
 
 VERSION, MAX_LAYERS, HEADER, LAYER_SLOTS, SAGE, GCN = 1, 4, 24, 32, 0, 1
 (H_VERSION, H_LAYERS, H_KIND, H_X0, H_LDX0, H_F0, H_HEAD_W, H_HEAD_B, H_HEAD_GW, H_HEAD_GB, H_CLASSES, H_LABELS,
- H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING, H_GRAD_EVENTS) = range(20)
+ H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING, H_GRAD_EVENTS, H_STAGE_EVENT,
+ H_STAGE_LAYER) = range(22)
 TIMING_SLOTS = 16
 (L_ROWPTR, L_COL, L_VAL, L_M, L_K, L_NNZ, L_TROWPTR, L_TCOL, L_TVAL, L_SAMPLED, L_NSAMPLED, L_RMAP, L_WW, L_BW,
  L_WB, L_BB, L_SCALE, L_OFFSET, L_GWW, L_GBW, L_GWB, L_GBB, L_GSCALE, L_GOFFSET, L_SEED) = range(25)
@@ -134,9 +135,11 @@ class NativeStep:
             stages.append([i for i, p in enumerate(self.params) if id(p) in mine])
         return stages
 
-    def step(self, x0, adjs, sampled_nodes, labels, grad_events=None) -> torch.Tensor:
+    def step(self, x0, adjs, sampled_nodes, labels, grad_events=None, stage_gate=None) -> torch.Tensor:
         """grad_events: optional [head event, layer 0 event, layer 1 event, ...] (torch.cuda.Event)
-        recorded on the step's stream once those gradients are final (GNN_SH_GRAD_EVENTS)."""
+        recorded on the step's stream once those gradients are final (GNN_SH_GRAD_EVENTS).
+        stage_gate: optional (torch.cuda.Event, layer): the event is recorded right after that
+        layer's forward aggregation (GNN_SH_STAGE_EVENT; staging.Stager waits on it)."""
         model = self.model
         training = model.training
         tr = bool(training and self.p_enc > 0)
@@ -171,6 +174,12 @@ class NativeStep:
                     ev.record()  # creates the underlying hipEvent; the step re-records it
                     E[1 + i] = ev.cuda_event
             d[H_GRAD_EVENTS] = E.ctypes.data
+        if stage_gate is not None:
+            ev, layer = stage_gate
+            if not getattr(ev, "_gnn_created", False):
+                ev.record()  # creates the underlying hipEvent once; the step re-records it
+                ev._gnn_created = True
+            d[H_STAGE_EVENT], d[H_STAGE_LAYER] = ev.cuda_event, int(layer)
         L = _lib.lib()
         dp = d.ctypes.data
         wsb = L.gnn_train_step_workspace_bytes(dp)

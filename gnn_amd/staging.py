@@ -159,6 +159,9 @@ class Stager:
         self.stream = torch.cuda.Stream(device=self.device)
         self.exchange = exchange
         self.timing: Optional[list] = None  # set to [] to record (event, event, bytes) per host copy
+        # optional torch.cuda.Event the staging kernels wait for (Trainer.stage_gate's event): the
+        # step re-records it after the gating layer's forward aggregation
+        self.gate: Optional[torch.cuda.Event] = None
 
     def take_timing(self):
         """(host bytes, seconds) summed over the recorded host-row copies; clears the record."""
@@ -209,6 +212,11 @@ class Stager:
             if self.timing is not None:
                 e1.record(st)
                 self.timing.append((e0, e1, plan.blob.nbytes if plan.blob is not None else nh * self.store.ld * 4))
+            if self.gate is not None:
+                # the uploads above go ahead at once (copy engine); the gathers and layer extractions
+                # below wait for the gate the step records after its layer-0 aggregation, so they run
+                # beside the MFMA-bound GEMMs and tails instead of competing for L2 with the gather
+                st.wait_event(self.gate)
             cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
             if nh and (plan.host_rows is not None or (plan.blob is not None and not self.store.zero_copy)):
                 cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
@@ -370,8 +378,9 @@ class PeerExchange:
             # always a group of its own: the negotiation may run on another thread
             # (NegotiatedStream) while this thread's row all-to-all / gradient all-reduce use
             # `group` — two threads on one communicator would interleave their collectives
-            with stdout_to_stderr():  # gloo prints its connection lines on stdout (bench: one JSON line)
-                meta_group = dist.new_group(backend="gloo")
+            from .train import new_gloo_group
+
+            meta_group = new_gloo_group()  # with the package's collective timeout
         self.meta_group = meta_group
 
     def prepare(self, plan: StagePlan) -> tuple:
@@ -466,8 +475,9 @@ class PeerDirect:
         self.verified_rows = 0  # rows read through the mappings and checked against the feature table
         mapped = []
         self._closer = weakref.finalize(self, _ipc_close_all, mapped, dev)
-        with stdout_to_stderr():
-            self.group = dist.new_group(backend="gloo")
+        from .train import new_gloo_group
+
+        self.group = new_gloo_group()
         err, info = "", None
         try:
             if buf.shape[0]:

@@ -63,6 +63,9 @@ class Trainer:
         self.world = 1
         if torch.distributed.is_available() and torch.distributed.is_initialized():
             self.world = torch.distributed.get_world_size(group)
+        # the data-parallel branch of step() (clip into the flat buffer, all-reduce, Adam on the
+        # sum): every N > 1 run; tests/test_rccl_gpu.py also drives it through a 1-rank RCCL group
+        self.dp = self.world > 1
         if self.world > 1:
             self.broadcast_parameters()
         # N > 1 with the executor: the gradient exchange bucketed per backward stage and started
@@ -78,6 +81,9 @@ class Trainer:
             except ValueError:
                 self.bucketed = None
         self.exchange = self.bucketed if os.environ.get("GNN_DP_BUCKETS", "0") == "1" else None
+        # (event, layer): recorded by the executor after that layer's forward aggregation; the
+        # staging of later batches waits on it (staging.Stager.gate, set by the caller)
+        self.stage_gate = None
 
     @property
     def num_params(self) -> int:
@@ -104,15 +110,16 @@ class Trainer:
         gradient and the same Adam update on every rank, all ranks must hold bit-identical
         parameters. Collective (every rank of the group). Returns {"identical", "digests"}."""
         d = self.param_digest()
-        if self.world <= 1:
+        dist = torch.distributed
+        if not (dist.is_available() and dist.is_initialized()):
             return {"identical": True, "digests": [d]}
-        digests = [None] * self.world
+        digests = [None] * dist.get_world_size(self.group)
         torch.distributed.all_gather_object(digests, d, group=self.group)
         return {"identical": all(x == digests[0] for x in digests), "digests": digests}
 
     def allreduce_grads(self) -> Optional[torch.Tensor]:
         """Σ over ranks of the (already clipped) gradients, in one flat buffer."""
-        if self.world <= 1:
+        if not self.dp:
             return None
         grads = [p.grad for p in self.params]
         flat = _flatten_dense_tensors(grads)
@@ -126,13 +133,15 @@ class Trainer:
             self.model.train()
         if self.executor is not None and self.executor.supports(x0, adjs, sampled_nodes, labels):
             if self.exchange is not None:  # buckets leave while the lower layers' backward runs
-                loss = self.executor.step(x0, adjs, sampled_nodes, labels, grad_events=self.exchange.events)
+                loss = self.executor.step(x0, adjs, sampled_nodes, labels, grad_events=self.exchange.events,
+                                          stage_gate=self.stage_gate)
                 self.exchange.issue()
                 self.exchange.finish()  # this rank's clip, Σ_r c_r g_r into the flat gradient
                 self.optimizer.step(clipped=True)
                 return loss
-            loss = self.executor.step(x0, adjs, sampled_nodes, labels)  # grads into the flat buffer
-            if self.world > 1:
+            loss = self.executor.step(x0, adjs, sampled_nodes, labels,  # grads into the flat buffer
+                                      stage_gate=self.stage_gate)
+            if self.dp:
                 flat = self.optimizer.clip_to_flat()
                 torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
                 self.optimizer.step(clipped=True)
@@ -155,7 +164,7 @@ class Trainer:
         else:
             loss.backward()
         if self.native:
-            if self.world > 1:
+            if self.dp:
                 flat = self.optimizer.clip_to_flat()  # this rank's clip, into the all-reduce buffer
                 torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
                 self.optimizer.step(clipped=True)
@@ -168,10 +177,55 @@ class Trainer:
         return loss.detach()
 
 
+DEFAULT_TIMEOUT_S = 180.0
+
+
+def collective_timeout():
+    """How long any collective of this package may wait for its peers (GNN_DIST_TIMEOUT_S,
+    default 180 s) before the rank fails. The reference's threads wait on a
+    ``threading.Barrier`` with no timeout (main.py:158,214), and torch's defaults are 10 min
+    (RCCL) and 30 min (gloo): a stalled collective must instead end the run, non-zero, well
+    inside a driver's time limit, with the rank and the call in the log."""
+    import datetime
+
+    s = float(os.environ.get("GNN_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    if not s > 0:
+        raise ValueError(f"GNN_DIST_TIMEOUT_S must be > 0, got {s}")
+    return datetime.timedelta(seconds=s)
+
+
+def init_group(backend: str, rank: Optional[int] = None, world: Optional[int] = None, local: int = 0):
+    """init_process_group with this package's collective timeout. RCCL ("nccl"): the watchdog's
+    asynchronous error handling stays on (TORCH_NCCL_ASYNC_ERROR_HANDLING, set to 1 = abort the
+    communicator and end the process unless the caller chose otherwise), so a collective that
+    does not complete within the timeout takes the rank down with the watchdog's report of the
+    rank, the operation and its sequence number instead of hanging; its heartbeat monitor is
+    held to the timeout + 60 s. gloo: every collective raises RuntimeError after the timeout."""
+    timeout = collective_timeout()
+    kw = {"timeout": timeout}
+    if rank is not None:
+        kw.update(rank=rank, world_size=world)
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        os.environ.setdefault("TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC", str(int(timeout.total_seconds()) + 60))
+        torch.distributed.init_process_group(backend, device_id=torch.device("cuda", local), **kw)
+    else:
+        from .staging import stdout_to_stderr
+
+        with stdout_to_stderr():  # gloo's connection lines go to stderr, not into the bench's stdout
+            torch.distributed.init_process_group(backend, **kw)
+
+
+def new_gloo_group():
+    """A gloo side group (host metadata, IPC handle exchange) with the same timeout."""
+    from .staging import stdout_to_stderr
+
+    with stdout_to_stderr():  # gloo prints its connection lines on stdout (bench: one JSON line)
+        return torch.distributed.new_group(backend="gloo", timeout=collective_timeout())
+
+
 def init_distributed(backend: Optional[str] = None):
     """Initialise torch.distributed from torchrun's environment; returns (rank, world, local_rank)."""
-    import os
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -182,11 +236,5 @@ def init_distributed(backend: Optional[str] = None):
             # box, gloo backend: RCCL refuses two ranks on one GPU) share them round-robin
             local = local % max(torch.cuda.device_count(), 1)
             torch.cuda.set_device(local)
-        if be == "nccl":
-            torch.distributed.init_process_group(be, device_id=torch.device("cuda", local))
-        else:
-            from .staging import stdout_to_stderr
-
-            with stdout_to_stderr():  # gloo's connection lines go to stderr, not into the bench's stdout
-                torch.distributed.init_process_group(be)
+        init_group(be, local=local)
     return rank, world, local

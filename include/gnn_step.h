@@ -26,7 +26,12 @@
  *     and optionally gradient-ready events: a HOST int64 array E, E[0] = entries, E[1] = a
  *     hipEvent_t recorded once the head's gradients are final, E[2 + l] = one recorded once
  *     layer l's gradients (weights, biases, scale, offset) are final (0 = none): the caller's
- *     data-parallel exchange starts on a bucket while the backward of the layers below runs.
+ *     data-parallel exchange starts on a bucket while the backward of the layers below runs;
+ *     and optionally a staging gate: a hipEvent_t (GNN_SH_STAGE_EVENT, 0 = none) recorded on the
+ *     step's stream right after layer GNN_SH_STAGE_LAYER's forward aggregation — the caller's
+ *     staging stream waits on it before the next batches' row gathers and layer extractions, so
+ *     those gather-bound kernels run beside the GEMMs and tails instead of competing with the
+ *     aggregation for L2 (main.py:129-137's staging, overlapped with the step).
  *   layer l: the operand A (rowptr / col / val, M x K, nnz) and its transpose (K x M, layers >= 1),
  *     sampled (int64 [M], SAGE) and rmap (int32 [K], rmap[sampled[i]] = i, SAGE layers >= 1),
  *     weights W_W / W_B (N x F row-major), biases, scale / offset, their gradient buffers, the
@@ -54,7 +59,8 @@ enum {
   GNN_SH_VERSION = 0, GNN_SH_LAYERS = 1, GNN_SH_KIND = 2, GNN_SH_X0 = 3, GNN_SH_LDX0 = 4, GNN_SH_F0 = 5,
   GNN_SH_HEAD_W = 6, GNN_SH_HEAD_B = 7, GNN_SH_HEAD_GW = 8, GNN_SH_HEAD_GB = 9, GNN_SH_CLASSES = 10,
   GNN_SH_LABELS = 11, GNN_SH_LDL = 12, GNN_SH_HEAD_SEED = 13, GNN_SH_PDROP_BITS = 14, GNN_SH_TRAINING = 15,
-  GNN_SH_LOSS = 16, GNN_SH_NHID = 17, GNN_SH_TIMING = 18, GNN_SH_GRAD_EVENTS = 19
+  GNN_SH_LOSS = 16, GNN_SH_NHID = 17, GNN_SH_TIMING = 18, GNN_SH_GRAD_EVENTS = 19, GNN_SH_STAGE_EVENT = 20,
+  GNN_SH_STAGE_LAYER = 21
 };
 enum {
   GNN_SL_ROWPTR = 0, GNN_SL_COL = 1, GNN_SL_VAL = 2, GNN_SL_M = 3, GNN_SL_K = 4, GNN_SL_NNZ = 5,

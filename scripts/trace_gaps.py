@@ -1,4 +1,4 @@
-"""Compute-stream gap analysis of a rocprofv3 kernel trace (scripts/gpu_trace.sh): per stream,
+"""Compute-stream gap analysis of a rocprofv3 kernel trace (scripts/gpu.sh ktrace step): per stream,
 busy time (union of kernel intervals) vs wall time over the steady-state window, and the largest
 idle gaps on the compute stream with the kernel that ended before / started after each gap.
 Usage: python scripts/trace_gaps.py kernel_trace.csv[.gz]"""

@@ -1,4 +1,4 @@
-"""Per-call breakdown of a rocprofv3 --kernel-trace CSV (scripts/gpu_trace.sh): the dispatches of
+"""Per-call breakdown of a rocprofv3 --kernel-trace CSV (scripts/gpu.sh ktrace step): the dispatches of
 the k-th to last training step (adam_kernel closes a step), with start offset, duration, queue,
 grid, and the compute queue's idle gaps. Usage: python scripts/trace_step.py TRACE.csv [k]"""
 import csv

@@ -61,6 +61,56 @@ def test_launch_world2_ok(tmp_path):
     assert "stdout goes to stderr" in r.stderr
 
 
+STALL_SCRIPT = textwrap.dedent("""
+    import os, sys, time
+    sys.path.insert(0, os.environ["GNN_TEST_REPO"])
+    import torch, torch.distributed as dist
+    from gnn_amd.train import init_distributed, new_gloo_group
+    rank, world, _ = init_distributed("gloo")
+    side = new_gloo_group() if sys.argv[1] == "side" else None
+    t = torch.ones(4)
+    dist.all_reduce(t, group=side)  # both ranks: the groups work
+    if rank == 1:
+        time.sleep(600)  # skips the next collective, alive (a stalled rank, not a dead one)
+    dist.all_reduce(t, group=side)  # rank 0 waits for rank 1: must fail after the timeout
+    print("unreachable", flush=True)
+""")
+
+
+@pytest.mark.parametrize("group", ["main", "side"])
+def test_stalled_collective_fails_the_run_within_the_timeout(tmp_path, group):
+    """A rank that never reaches a collective must end the run non-zero within the collective
+    timeout (GNN_DIST_TIMEOUT_S) plus the launcher's grace, naming the rank and the call — on the
+    default group and on a gloo side group alike (the reference's Barrier waits forever,
+    main.py:158,214; torch's defaults are 10 / 30 min)."""
+    script = tmp_path / "stall.py"
+    script.write_text(STALL_SCRIPT)
+    code = ("import sys; sys.path.insert(0, %r); from gnn_amd import launch; "
+            "sys.exit(launch.launch([sys.executable, %r, %r], 2, grace_s=3.0))" % (REPO, str(script), group))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GNN_LAUNCHED_BY")}
+    env.update(GNN_DIST_TIMEOUT_S="4", GNN_TEST_REPO=REPO)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=170, env=env)
+    dt = time.monotonic() - t0
+    assert r.returncode not in (0, None), r.stderr[-3000:]
+    assert "unreachable" not in r.stdout
+    assert "rank 0 exited with" in r.stderr, r.stderr[-3000:]
+    assert "all_reduce" in r.stderr  # the traceback names the call that timed out
+    assert dt < 4 + 3 + 60, dt  # timeout + grace + two interpreters' start-up
+
+
+def test_collective_timeout_env(monkeypatch):
+    from gnn_amd import train
+
+    monkeypatch.delenv("GNN_DIST_TIMEOUT_S", raising=False)
+    assert train.collective_timeout().total_seconds() == train.DEFAULT_TIMEOUT_S <= 180
+    monkeypatch.setenv("GNN_DIST_TIMEOUT_S", "7.5")
+    assert train.collective_timeout().total_seconds() == 7.5
+    monkeypatch.setenv("GNN_DIST_TIMEOUT_S", "0")
+    with pytest.raises(ValueError):
+        train.collective_timeout()
+
+
 def test_launch_failing_rank_stops_the_others(tmp_path):
     r, dt = _driver(tmp_path, "fail")
     assert r.returncode == 7, (r.returncode, r.stderr[-2000:])
