@@ -25,11 +25,12 @@ int launch_scan_exclusive(const int* in, int n, int* out, hipStream_t st);
 bool spmm_row_chain(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t ldx, int64_t ldy, const void* X,
                     const void* Y);
 
-// gnn_gemm_f32_split3 with the split-k choice made for a batch of split_nbatch products
-// (gemm.hip): one product of a batch launched on its own, bit-identical to the batched result.
+// gnn_gemm_f32_split3 with the split-k and tail-tile choices made for a batch of split_nbatch
+// products (gemm.hip): product batch_index of that batch launched on its own (nbatch = 1),
+// bit-identical to its result in the batched launch.
 int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, int split_nbatch,
-                         const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
-                         int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
+                         int batch_index, const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                         float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream);
 
 // gnn_gemm_f32_split3 with row-indexed operands: A's row m is A[ia[b][m]] (m-major A, a_rows
 // source rows), B's row k is B[ib[b][k]] (k-major B, b_rows source rows); NULL arrays / entries:

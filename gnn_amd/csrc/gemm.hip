@@ -645,7 +645,8 @@ __global__ __launch_bounds__(256) void gemm_tail_reduce_kernel(Batch bt, const f
 // bf16, rows and k zero-padded to 128 / 16, so a thread's 16 bytes of (row, k half) are one
 // coalesced load and the GEMM needs no guards. The pieces are the split3 kernel's (truncation,
 // exact) and the MFMA schedule is the same (same k16 steps, same six products in the same
-// order): results bit-identical to gnn_gemm_f32_split3.
+// order): results bit-identical to gnn_gemm_f32_split3 on shapes without split3's tail tiles
+// (tail_plan; with GNN_GEMM_TAIL=0 on every shape).
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ void split_piece8(const float v[8], u4v& ph, u4v& pm, u4v& pl) {
 #pragma unroll
@@ -879,9 +880,13 @@ struct RowIndex {
   int64_t b_rows = 0;
 };
 
+// batch_index (with split_nbatch > 0): which product of the mimicked batch this launch is, so that
+// its tiles that the batched launch would run as tail pieces (tail_plan over the whole batch) run
+// as the same pieces here — the same sums, bit for bit.
 int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, const float* const* A,
              int64_t lda, const float* const* B, int64_t ldb, float* const* C, int64_t ldc, void* workspace,
-             size_t workspace_bytes, void* stream, int split_nbatch = 0, const RowIndex* ri = nullptr) {
+             size_t workspace_bytes, void* stream, int split_nbatch = 0, const RowIndex* ri = nullptr,
+             int batch_index = -1) {
   GNN_REQUIRE(M >= 0 && N >= 0 && K >= 0, "gnn_gemm_f32: negative size");
   GNN_REQUIRE(M < INT_MAX && N < INT_MAX && K < INT_MAX, "gnn_gemm_f32: sizes must be < 2^31");
   GNN_REQUIRE(nbatch >= 1 && nbatch <= MAX_BATCH, "gnn_gemm_f32: nbatch must be 1..%d", MAX_BATCH);
@@ -926,6 +931,20 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
     if (const char* e = getenv("GNN_GEMM_BKT")) bkt = atoi(e) == 16 ? 16 : 32;  // experiments
   TailPlan tp;
   if (algo == ALGO_S3 && splits == 1 && split_nbatch == 0 && K > 0 && tail_enabled()) tp = tail_plan(M, N, K, nbatch);
+  if (algo == ALGO_S3 && splits == 1 && split_nbatch > 0 && nbatch == 1 && batch_index >= 0 && K > 0 &&
+      tail_enabled()) {
+    // one product of a batch of split_nbatch, launched alone: the batch's tail tiles that are this
+    // product's tiles [batch_index * T1, (batch_index + 1) * T1) run as the same k pieces
+    const TailPlan full = tail_plan(M, N, K, split_nbatch);
+    const int64_t T1 = ceil_div(M, (int64_t)BM) * ceil_div(N, (int64_t)BN);
+    const int64_t lo = (int64_t)batch_index * T1;
+    if (full.s > 0 && full.base < lo + T1) {
+      tp.base = (int)std::max<int64_t>(0, full.base - lo);
+      tp.s = full.s;
+      tp.rem = (int)(T1 - tp.base);
+      if (tp.base % 8) xcdm = 0;  // the kernel's XCD map of the whole tiles needs base % 8 == 0 (speed only)
+    }
+  }
   int klen = splits > 1 ? (int)(ceil_div(ceil_div(K, (int64_t)splits), (int64_t)bkt) * bkt) : (int)K;
   if (tp.s > 0) klen = (int)(ceil_div(ceil_div(K, (int64_t)tp.s), (int64_t)bkt) * bkt);
   if (splits > 1 || tp.s > 0) {
@@ -1113,10 +1132,10 @@ int gnn_gemm_f32_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N
 namespace gnn {
 
 int gemm_split3_as_batch(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch, int split_nbatch,
-                         const float* const* A, int64_t lda, const float* const* B, int64_t ldb, float* const* C,
-                         int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
+                         int batch_index, const float* const* A, int64_t lda, const float* const* B, int64_t ldb,
+                         float* const* C, int64_t ldc, void* workspace, size_t workspace_bytes, void* stream) {
   return gemm_run(ALGO_S3, a_kmajor, b_kmajor, M, N, K, nbatch, A, lda, B, ldb, C, ldc, workspace, workspace_bytes,
-                  stream, split_nbatch);
+                  stream, split_nbatch, nullptr, batch_index);
 }
 
 int gemm_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t K, int nbatch,

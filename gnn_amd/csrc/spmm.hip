@@ -528,7 +528,7 @@ template <typename CT>
 __device__ void build_operand_row(const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
                                   const CT* __restrict__ colidx, const float* __restrict__ normfact, int r,
                                   int* __restrict__ out_col, float* __restrict__ out_val, int* sk, float* sv,
-                                  int lane) {
+                                  int lane, unsigned long long* __restrict__ dflag, unsigned long long gen) {
   const int b = rowptr[r];
   const int e = rowptr[r + 1];
   if (b == e) return;
@@ -558,6 +558,9 @@ __device__ void build_operand_row(const int* __restrict__ fullrowptr, const int*
       out_col[b + lane] = k;
       out_val[b + lane] = v;
     }
+    // a repeated column, adjacent once sorted: flagged for the caller's lazy coalesce
+    const int kn = __shfl_down(k, 1);
+    if (dflag && __ballot(lane + 1 < L && k == kn) != 0ull && lane == 0) atomicMax(dflag, gen);
     return;
   }
   // Longer unsorted rows (never produced by scipy slicing, kept for generality): bitonic
@@ -604,12 +607,17 @@ __device__ void build_operand_row(const int* __restrict__ fullrowptr, const int*
       __builtin_amdgcn_wave_barrier();
     }
   }
+  bool dup = false;
   if (L <= SEG_WAVE_LDS) {
     for (int i = lane; i < L; i += 64) {
       out_col[b + i] = sk[i];
       out_val[b + i] = sv[i];
+      dup |= i + 1 < L && sk[i] == sk[i + 1];
     }
+  } else {
+    for (int i = lane; i + 1 < L; i += 64) dup |= out_col[b + i] == out_col[b + i + 1];
   }
+  if (dflag && __ballot(dup) != 0ull && lane == 0) atomicMax(dflag, gen);
 }
 
 // Row-per-wave build with the sort fallback; grid-stride over rows. With `flag`, a no-op
@@ -619,14 +627,15 @@ __global__ __launch_bounds__(256) void build_operand_kernel(
     const int* __restrict__ fullrowptr, const int* __restrict__ rowptr,
     const CT* __restrict__ colidx, const float* __restrict__ normfact, int nrows,
     int* __restrict__ out_col, float* __restrict__ out_val,
-    const unsigned long long* __restrict__ flag, unsigned long long gen) {
+    unsigned long long* __restrict__ flag, unsigned long long gen) {
   __shared__ int sk[4][SEG_WAVE_LDS];
   __shared__ float sv[4][SEG_WAVE_LDS];
-  if (flag && *flag < gen) return;
+  if (flag && flag[0] < gen) return;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   for (int r = blockIdx.x * 4 + w; r < nrows; r += gridDim.x * 4)
-    build_operand_row<CT>(fullrowptr, rowptr, colidx, normfact, r, out_col, out_val, sk[w], sv[w], lane);
+    build_operand_row<CT>(fullrowptr, rowptr, colidx, normfact, r, out_col, out_val, sk[w], sv[w], lane,
+                          flag ? flag + 1 : nullptr, gen);
 }
 
 // nonzeros per wave in the flat operand builders (a multiple of 64)
@@ -657,7 +666,7 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
   const int nin = __popcll(__ballot(e < ce));
   int rl = rf;
   if (nin == 64) rl = wave_first_true(rf, nrows, lane, [&](int r) { return rowptr[r + 1] >= ce; });
-  bool bad = false;
+  bool bad = false, dup = false;
 #pragma unroll
   for (int t = 0; t < BUILD_CHUNK / 64; ++t) {
     const int i = cs + t * 64 + lane;
@@ -677,13 +686,19 @@ __global__ __launch_bounds__(256) void build_operand_flat_kernel(
         end = rowptr[lo + 1];
       }
       const int c = (int)colidx[i];
-      if (i + 1 < end) bad |= c > (int)colidx[i + 1];
+      if (i + 1 < end) {
+        const int cn = (int)colidx[i + 1];
+        bad |= c > cn;
+        dup |= c == cn;
+      }
       const double inv = 1.0 / (double)(fullrowptr[lo + 1] - fullrowptr[lo]);
       out_col[i] = c;
       out_val[i] = (float)(inv * (double)normfact[c]);
     }
   }
   if (flag && __ballot(bad) != 0ull && lane == 0) atomicMax(flag, gen);
+  // word 1: a repeated column in an already ascending row (unsorted rows: checked after their sort)
+  if (flag && __ballot(dup) != 0ull && lane == 0) atomicMax(flag + 1, gen);
 }
 
 // Values of the transposed operand from its CSR structure (the CSC of A): entry i of
@@ -1642,9 +1657,10 @@ int gnn_build_operand_f32(const int32_t* fullrowptr, const int32_t* rowptr, cons
                           const float* normfact, int64_t nrows, int64_t ncols, int64_t nnz, int32_t* csr_col,
                           float* csr_val, int64_t* coo_indices, void* workspace, size_t workspace_bytes,
                           void* stream) {
-  // the "unsorted row seen" word lives in the caller's workspace, zeroed on the call's stream:
-  // no allocation inside the library, no state shared between concurrent calls
-  GNN_REQUIRE(nrows == 0 || nnz == 0 || (workspace != nullptr && workspace_bytes >= 8 && (uintptr_t)workspace % 8 == 0),
+  // the "unsorted row seen" and "repeated column seen" words live in the caller's workspace,
+  // zeroed on the call's stream: no allocation inside the library, no state shared between
+  // concurrent calls
+  GNN_REQUIRE(nrows == 0 || nnz == 0 || (workspace != nullptr && workspace_bytes >= 16 && (uintptr_t)workspace % 8 == 0),
               "gnn_build_operand_f32: needs an 8-byte aligned workspace of gnn_build_operand_workspace_bytes() bytes");
   return build_operand(fullrowptr, rowptr, colidx, colidx_bytes, normfact, nrows, ncols, nnz, csr_col, csr_val,
                        coo_indices, (unsigned long long*)workspace, stream);
@@ -1674,7 +1690,7 @@ int build_operand(const int32_t* fullrowptr, const int32_t* rowptr, const void* 
   const dim3 grid((unsigned)ceil_div(nrows, 4));
   const bool sorted = flag == nullptr;
   const unsigned long long gen = 1;
-  if (!sorted) GNN_HIP(hipMemsetAsync(flag, 0, sizeof(*flag), st), "operand flag memset");
+  if (!sorted) GNN_HIP(hipMemsetAsync(flag, 0, 2 * sizeof(*flag), st), "operand flag memset");
   const dim3 gflat((unsigned)ceil_div(nnz, 4 * BUILD_CHUNK));  // 4 waves x BUILD_CHUNK nonzeros
   const dim3 gfix(16);  // usually a no-op (gated): keep the launch small
   switch (colidx_bytes) {

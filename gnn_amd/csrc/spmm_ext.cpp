@@ -118,7 +118,7 @@ at::Tensor spmm_load_balance(const at::Tensor& sparseMat, const at::Tensor& dens
 
 // spmm.cpp:44-50 -> cuda_spmm.cu:787-827: val = (float)((1.0/deg_full(row)) * (double)normfact[col]),
 // a coalesced sparse COO (int64 indices [2, nnz], float32 values) of shape (nrows, ncols).
-at::Tensor create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& rowptr, const at::Tensor& colidx,
+py::object create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& rowptr, const at::Tensor& colidx,
                              const at::Tensor& normfact, int64_t nrows, int64_t ncols) {
   for (const at::Tensor* t : {&fullrowptr, &rowptr, &colidx, &normfact})
     TORCH_CHECK(t->is_cuda(), "create_coo_tensor inputs must be CUDA tensors");
@@ -140,13 +140,32 @@ at::Tensor create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& row
                                  nf.data_ptr<float>(), nrows, ncols, nnz, col32.data_ptr<int32_t>(), val.data_ptr<float>(),
                                  idx.data_ptr<int64_t>(), ws.data_ptr(), wsb, current_stream(ci)),
            "gnn_build_operand_f32");
-  at::Tensor out = at::_sparse_coo_tensor_unsafe(idx, val, {nrows, ncols}, nf.options());
-  // Columns come out ascending per row; a repeated (row, col) pair (never made by the reference's
-  // samplers) is summed as the reference's .coalesce() does (cuda_spmm.cu:825), so a tensor
-  // flagged coalesced really is (one small check, synchronising as the reference's coalesce does).
-  if (nnz > 1 && at::eq(idx.narrow(1, 1, nnz - 1), idx.narrow(1, 0, nnz - 1)).all(0).any().item<bool>())
-    return out.coalesce();
-  return out._coalesced_(true);
+  at::Tensor out = at::_sparse_coo_tensor_unsafe(idx, val, {nrows, ncols}, nf.options())._coalesced_(true);
+  // Columns come out ascending per row. A repeated (row, col) pair (never made by the reference's
+  // samplers) is flagged by the builder on the GPU (the workspace's second word) without a host
+  // read here — the call stays stream-ordered and graph-capturable; the first spmm_load_balance on
+  // the tensor reads the flag and, if set, sums the duplicates in place as the reference's
+  // .coalesce() does (cuda_spmm.cu:825).
+  py::object t = py::cast(out);
+  if (nrows > 0 && nnz > 1) t.attr("_gnn_dup") = py::cast(ws.view(at::kLong).narrow(0, 1, 1));
+  return t;
+}
+
+// The deferred half of create_coo_tensor's coalesce (above): read the repeated-column flag once
+// (one synchronisation, as the reference's coalesce) and coalesce the tensor in place if set.
+at::Tensor resolve_duplicates(const py::object& sparse) {
+  at::Tensor sp = sparse.cast<at::Tensor>();
+  if (!py::hasattr(sparse, "_gnn_dup")) return sp;
+  py::object w = sparse.attr("_gnn_dup");
+  if (w.is_none()) return sp;
+  sparse.attr("_gnn_dup") = py::none();
+  if (w.cast<at::Tensor>().item<int64_t>() != 0)
+    sp.copy_(at::_sparse_coo_tensor_unsafe(sp._indices(), sp._values(), sp.sizes()).coalesce());
+  return sp;
+}
+
+at::Tensor spmm_load_balance_py(const py::object& sparseMat, const at::Tensor& denseMat) {
+  return spmm_load_balance(resolve_duplicates(sparseMat), denseMat);
 }
 
 }  // namespace
@@ -166,9 +185,9 @@ TORCH_LIBRARY_IMPL(gnn, CUDA, m) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) sparse aggregation: the reference's `spmm` module over libgnn_spmm.so";
-  m.def("spmm_load_balance", &spmm_load_balance, "Y = A·X (A sparse COO, coalesced; X dense) on the GPU",
+  m.def("spmm_load_balance", &spmm_load_balance_py, "Y = A·X (A sparse COO, coalesced; X dense) on the GPU",
         py::arg("sparseMat"), py::arg("denseMat"));
-  m.def("spmm_naive", &spmm_load_balance, "same as spmm_load_balance (one kernel serves both, spmm.cpp:38-42)",
+  m.def("spmm_naive", &spmm_load_balance_py, "same as spmm_load_balance (one kernel serves both, spmm.cpp:38-42)",
         py::arg("sparseMat"), py::arg("denseMat"));
   m.def("create_coo_tensor", &create_coo_tensor, "sampled-adjacency builder (spmm.cpp:44-50)", py::arg("fullrowptr"),
         py::arg("rowptr"), py::arg("colidx"), py::arg("normfact"), py::arg("nrows"), py::arg("ncols"));

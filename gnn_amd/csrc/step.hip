@@ -203,11 +203,8 @@ bool small_overlap_enabled() {
 }
 
 bool overlap_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("GNN_STEP_OVERLAP");
-    return e && atoi(e) != 0;
-  }();
-  return on;
+  const char* e = getenv("GNN_STEP_OVERLAP");  // read per step (tests toggle it in-process)
+  return e && atoi(e) != 0;
 }
 
 // Row-major products on rocBLAS (column-major underneath): the small layer-2 / head products.
@@ -441,7 +438,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       const float* Ab[1] = {b.xs};
       const float* Bb[1] = {WB};
       float* Cb[1] = {b.hB};
-      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, Ab, b.ldo, Bb, b.F, Cb, N, b.ws_gemm_f2, b.b_gemm_f,
+      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, 0, Ab, b.ldo, Bb, b.F, Cb, N, b.ws_gemm_f2, b.b_gemm_f,
                                         aux->s));
       arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
       GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
@@ -451,7 +448,7 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       const float* Aw[1] = {b.feat};
       const float* Bw[1] = {WW};
       float* Cw[1] = {b.hW};
-      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, Aw, b.ldo, Bw, b.F, Cw, N, b.ws_gemm_f, b.b_gemm_f, st));
+      GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, 1, Aw, b.ldo, Bw, b.F, Cw, N, b.ws_gemm_f, b.b_gemm_f, st));
       GNN_TRY(fork_join(aux, aux->s, st));
     } else if (small_side) {
       b.xs_gathered = true;

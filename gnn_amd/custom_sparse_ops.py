@@ -115,7 +115,7 @@ class CsrOperand:
     rowptr int32[M+1], col int32[nnz], val fp32[nnz], columns ascending inside each row.
     ``transpose()`` returns (and caches) the canonical CSR of Aᵀ (K x M)."""
 
-    __slots__ = ("rowptr", "col", "val", "shape", "nnz", "_t", "_tw", "__weakref__")
+    __slots__ = ("rowptr", "col", "val", "shape", "nnz", "_t", "_tw", "_dup_word", "__weakref__")
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, shape: Tuple[int, int]):
         self.rowptr = rowptr
@@ -126,6 +126,7 @@ class CsrOperand:
         self._t: Optional["CsrOperand"] = None  # the cached transpose (strong)
         self._tw = None  # on a transpose: weakref back to the operand it was made from (no cycle,
         # so refcounting frees an operand pair as soon as the staged batch drops it)
+        self._dup_word = None  # create_coo_tensor: the builder's repeated-column word (device int64)
 
     @property
     def device(self) -> torch.device:
@@ -173,10 +174,28 @@ class CsrOperand:
         return torch.sparse_coo_tensor(idx, self.val, self.shape, is_coalesced=True)
 
 
+def _resolve_duplicates(mat: torch.Tensor) -> None:
+    """create_coo_tensor's deferred half of the reference's .coalesce() (cuda_spmm.cu:825): the
+    builder flags a repeated (row, col) pair on the GPU (the second word of its workspace) and
+    the returned tensor is marked coalesced without a host read; the first aggregation on the
+    tensor reads that word (one synchronisation, like the reference's coalesce) and, if it is
+    set, coalesces the tensor in place (the duplicates summed, nnz shrinks) and drops the CSR
+    image built from the uncoalesced entries."""
+    word = mat._gnn_dup
+    mat._gnn_dup = None
+    if int(word.item()) == 0:
+        return
+    coal = torch.sparse_coo_tensor(mat._indices(), mat._values(), mat.shape).coalesce()
+    mat.copy_(coal)
+    mat._gnn_csr = None
+
+
 def csr_of(mat: "torch.Tensor | CsrOperand") -> CsrOperand:
     """CSR image of a sampled operand: cached one, or built on the GPU from a coalesced COO."""
     if isinstance(mat, CsrOperand):
         return mat
+    if getattr(mat, "_gnn_dup", None) is not None:
+        _resolve_duplicates(mat)
     plan = getattr(mat, "_gnn_csr", None)
     if plan is not None:
         return plan
@@ -349,12 +368,15 @@ def build_operand(fullrowptr: torch.Tensor, rowptr: torch.Tensor, colidx: torch.
                 nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _stream(dev)), "gnn_build_operand_sorted_f32")
         else:
             wsb = _lib.lib().gnn_build_operand_workspace_bytes()
-            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)  # the unsorted-row flag
+            ws = torch.empty(wsb, dtype=torch.uint8, device=dev)  # the unsorted-row and repeated-column words
             _lib.check(_lib.lib().gnn_build_operand_f32(
                 _ptr(fullrowptr), _ptr(rowptr), _ptr(colidx), colidx.element_size(), _ptr(normfact),
                 nrows, ncols, nnz, _ptr(col32), _ptr(val), _ptr(coo), _ptr(ws), wsb, _stream(dev)),
                 "gnn_build_operand_f32")
-    return CsrOperand(rowptr, col32, val, (nrows, ncols)), coo
+    op = CsrOperand(rowptr, col32, val, (nrows, ncols))
+    if not sorted_rows and nrows > 0 and nnz > 1:
+        op._dup_word = ws.view(torch.int64)[1:2]  # set on the GPU iff a row repeats a column
+    return op, coo
 
 
 def extract_operand(graph, rows: torch.Tensor, cols: torch.Tensor, normfact: torch.Tensor, nnz: int,
@@ -452,13 +474,14 @@ def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> tor
     if all(isinstance(t, torch.Tensor) and t.device.type == "cpu" for t in ins):
         return _create_coo_tensor_cpu(*ins, int(nrows), int(ncols))
     op, coo = build_operand(fullrowptr, rowptr, colidx, normfact, int(nrows), int(ncols), with_coo=True)
-    if coo.shape[1] > 1 and bool(((coo[:, 1:] == coo[:, :-1]).all(0)).any()):
-        # a repeated column within a row (the reference's samplers never make one: LADIES' after
-        # nodes are unique, sampler.py:135-139): sum the duplicates as the reference's .coalesce()
-        # does (cuda_spmm.cu:825); the CSR image is then rebuilt from the coalesced tensor
-        return torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols))).coalesce()
     t = torch.sparse_coo_tensor(coo, op.val, (int(nrows), int(ncols)), is_coalesced=True)
     t._gnn_csr = op
+    # A repeated column within a row (the reference's samplers never make one: LADIES' after nodes
+    # are unique, sampler.py:135-139) is flagged by the builder on the GPU; no host read here (the
+    # call stays stream-ordered and graph-capturable): the first aggregation on the tensor reads
+    # the flag and, if set, sums the duplicates in place as the reference's .coalesce() does
+    # (cuda_spmm.cu:825; _resolve_duplicates).
+    t._gnn_dup = getattr(op, "_dup_word", None)
     return t
 
 

@@ -102,7 +102,9 @@ int gnn_gemm_f32_split3_indexed(int a_kmajor, int b_kmajor, int64_t M, int64_t N
  * zero-padded planes [piece][k tile of 16][R rounded up to 128][16] bf16
  * (gnn_gemm_p3_packed_bytes(R, K) bytes, 16-byte aligned); gnn_gemm_p3 then computes
  * C[b] (M x N, row stride ldc) = A[b] · B[b]ᵀ-as-packed with the split3 kernel's tile, k steps
- * and MFMA order: bit-identical to gnn_gemm_f32_split3 on the same operands. */
+ * and MFMA order: bit-identical to gnn_gemm_f32_split3 on the same operands for shapes without
+ * split3's tail tiles (gnn_gemm_f32_split3 sums the last 1-32 tiles past a multiple of 256 as k
+ * pieces when GNN_GEMM_TAIL is on; p3 has no tail mode — equal there with GNN_GEMM_TAIL=0). */
 size_t gnn_gemm_p3_packed_bytes(int64_t R, int64_t K);
 int gnn_gemm_p3_pack_f32(const float* src, int64_t ld, int kmajor, const int64_t* idx, int64_t R, int64_t K,
                          void* out, size_t out_bytes, void* stream);

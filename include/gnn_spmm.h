@@ -104,11 +104,15 @@ void gnn_spmm_set_timing_events(void* start, void* stop);
  * colidx may be int16 (colidx_bytes = 2, sign-extended like the reference's int16
  * accessor), int32 (4) or int64 (8). Rows whose columns are not ascending are sorted
  * (key = column, payload = value), which is what the reference's .coalesce() does
- * (cuda_spmm.cu:825); rows are assumed free of duplicate columns (scipy slicing output).
+ * (cuda_spmm.cu:825). A repeated column within a row (never made by scipy slicing or the
+ * reference's samplers) is NOT merged here — merging changes nnz, which the host would have to
+ * read back — but flagged: the workspace's second int64 word is nonzero after the call iff a row
+ * repeats a column (checked after sorting), so a caller can coalesce lazily at a point that
+ * synchronises anyway (gnn_amd.custom_sparse_ops: the first aggregation on the tensor).
  * Outputs: csr_col (int32, nnz), csr_val (fp32, nnz) and, if coo_indices != NULL, the
  * coalesced COO indices int64[2][nnz] (row-major: all rows then all columns).
  * `workspace` (device, 8-byte aligned, >= gnn_build_operand_workspace_bytes()) holds the
- * call's "unsorted row seen" word, zeroed on `stream` by the call itself: the library keeps
+ * call's "unsorted row seen" and "repeated column seen" words, zeroed on `stream` by the call itself: the library keeps
  * no device state and allocates nothing, so the call is graph-capturable and concurrent
  * calls on different streams need different workspaces.
  * ------------------------------------------------------------------------------- */

@@ -157,3 +157,41 @@ def test_folded_layer2_backward_is_bit_identical(dev, monkeypatch):
             assert _rel(x, y) <= 1e-5, ("gradient differs (default grid)", s, i, _rel(x, y))
         for i in range(6 if s == 0 else 0):  # first step's layer 0: unaffected by the column-sum grouping
             assert torch.equal(gc[s][i], gb[s][i]), ("layer-0 gradient differs (default grid)", s, i)
+
+
+def test_stream_overlap_variants_are_bit_identical(dev, monkeypatch):
+    """The executor's stream forks are schedule-only: the top layer's small products on
+    the aux stream (GNN_STEP_SMALL_OVERLAP, default on) vs all on the step's stream; the big layers'
+    x[sampled] products beside their aggregations (GNN_STEP_OVERLAP=1: each product of the pair
+    launched alone by gemm_split3_as_batch, which must then sum exactly as the batched launch —
+    including the layer-1 forward's split3 tail tiles, 544 = 2 x 256 + 32); and the gradient-ready
+    events of the bucketed DP exchange recorded (GNN_SH_GRAD_EVENTS). Loss and every gradient must
+    be bit-identical over two Adam steps."""
+    model_name, F, ncls, db, x0 = _batch("reddit_sage", dev)
+    variants = [{}, {"GNN_STEP_SMALL_OVERLAP": "0"}, {"GNN_STEP_OVERLAP": "1"},
+                {"GNN_STEP_OVERLAP": "1", "GNN_STEP_SMALL_OVERLAP": "0"}, {"events": True}]
+    res = []
+    for v in variants:
+        for k in ("GNN_STEP_SMALL_OVERLAP", "GNN_STEP_OVERLAP"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in v.items():
+            if k != "events":
+                monkeypatch.setenv(k, val)
+        tr = _trainer(model_name, F, ncls, dev, native=True)
+        if v.get("events"):
+            evs = [torch.cuda.Event() for _ in range(4)]
+            step = tr.executor.step
+            tr.executor.step = lambda *a, **kw: step(*a, grad_events=evs, **kw)
+        losses, grads = [], []
+        for it in range(2):
+            torch.manual_seed(100 + it)
+            losses.append(float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels)))
+            grads.append([p.grad.detach().clone() for p in tr.params])
+        torch.cuda.synchronize()
+        res.append((losses, grads))
+    l0, g0 = res[0]
+    for v, (l, g) in zip(variants[1:], res[1:]):
+        assert l == l0, (v, l, l0)
+        for s in range(2):
+            for i, (x, y) in enumerate(zip(g[s], g0[s])):
+                assert torch.equal(x, y), ("gradient differs", v, s, i)

@@ -520,15 +520,51 @@ def test_config2_full_size_forward_and_backward(dev):
 
 
 def test_create_coo_tensor_sums_duplicate_columns(dev):
+    """A repeated (row, col) pair is summed as the reference's .coalesce() does (cuda_spmm.cu:825):
+    flagged by the builder on the GPU, merged in place by the first aggregation on the tensor (the
+    call itself reads nothing back: test_create_coo_tensor_graph_capture)."""
     M, K, full, rowptr, col, nf = duplicate_columns_case()
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    A = cso.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int16)), t(nf), M, K)
     ref = coalesced_reference(M, K, full, rowptr, col, nf)
-    assert A.is_coalesced() and A._nnz() == ref._nnz() == 10
-    assert torch.equal(A._indices().cpu(), ref._indices())
-    np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
     X = torch.randn(K, 40, device=dev)
-    np.testing.assert_allclose(cso.spmm(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(), rtol=RTOL, atol=ATOL)
+    for ctype in (np.int16, np.int32):  # sorted rows with a repeat (flat pass) / the same rows reversed (fix pass)
+        for rev in (False, True):
+            c = col.copy()
+            if rev:
+                for r in range(M):
+                    c[rowptr[r]:rowptr[r + 1]] = c[rowptr[r]:rowptr[r + 1]][::-1]
+            A = cso.create_coo_tensor(t(full), t(rowptr), t(c.astype(ctype)), t(nf), M, K)
+            assert A.is_coalesced()
+            Y = cso.spmm(A, X)
+            assert A._nnz() == ref._nnz() == 10
+            assert torch.equal(A._indices().cpu(), ref._indices())
+            np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
+            np.testing.assert_allclose(Y.cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(), rtol=RTOL, atol=ATOL)
+
+
+def test_create_coo_tensor_graph_capture(dev):
+    """create_coo_tensor issues no host read (the drop-in builder synced per call for its
+    duplicate check): it captures into a HIP graph, and replays rebuild the operand bit-exactly
+    (the oracle's create_coo_tensor restatement), with and without an unsorted row."""
+    rng = np.random.default_rng(11)
+    M, K = 200, 300
+    lens = rng.integers(0, 40, M)
+    full, rowptr, col, nf = random_csr(M, K, lens, rng)
+    col = col.copy()
+    col[rowptr[3]:rowptr[4]] = col[rowptr[3]:rowptr[4]][::-1]  # an unsorted row (the fix pass runs)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ins = (t(full), t(rowptr), t(col.astype(np.int32)), t(nf))
+    cso.create_coo_tensor(*ins, M, K)  # warm-up outside the capture (library load, allocator)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        A = cso.create_coo_tensor(*ins, M, K)
+    g.replay()
+    torch.cuda.synchronize()
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    assert np.array_equal(A._gnn_csr.col.cpu().numpy(), ocol)
+    assert np.array_equal(A._gnn_csr.val.cpu().numpy(), oval)
+    assert int(A._gnn_dup.item()) == 0
 
 
 # ---- small operands: spmm_row_kernel (a workgroup of WPR waves per (row, column slice)) ----

@@ -187,9 +187,35 @@ def test_module_create_coo_tensor_sums_duplicate_columns(dev):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     A = mod.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int32)), t(nf), M, K)
     ref = coalesced_reference(M, K, full, rowptr, col, nf)
-    assert A.is_coalesced() and A._nnz() == 10
+    assert A.is_coalesced()
+    X = torch.randn(K, 40, device=dev)
+    Y = mod.spmm_load_balance(A, X)  # the first aggregation merges the flagged repeat in place
+    assert A._nnz() == 10
     assert torch.equal(A._indices().cpu(), ref._indices())
     np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
-    X = torch.randn(K, 40, device=dev)
-    np.testing.assert_allclose(mod.spmm_load_balance(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(),
-                               rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(Y.cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_module_create_coo_tensor_graph_capture(dev):
+    """The module's create_coo_tensor reads nothing back (no duplicate check on the host): it
+    captures into a HIP graph and the replay builds the reference's values bit for bit."""
+    import oracle as O
+    from oracle.fixtures import random_csr
+
+    mod = torch_ops.load()
+    rng = np.random.default_rng(12)
+    M, K = 150, 260
+    full, rowptr, col, nf = random_csr(M, K, rng.integers(0, 30, M), rng)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ins = (t(full), t(rowptr), t(col.astype(np.int16)), t(nf))
+    mod.create_coo_tensor(*ins, M, K)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        A = mod.create_coo_tensor(*ins, M, K)
+    g.replay()
+    torch.cuda.synchronize()
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    assert np.array_equal(A._indices()[1].cpu().numpy(), ocol)
+    assert np.array_equal(A._values().cpu().numpy(), oval)
