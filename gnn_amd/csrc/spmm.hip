@@ -22,6 +22,7 @@
 //    before the FMAs (memory-level parallelism for an HBM/Infinity-Cache bound gather).
 //  * Everything is stream-ordered on the caller's stream: no host syncs, no allocation.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <climits>
 #include <cstdarg>
@@ -469,7 +470,7 @@ __global__ __launch_bounds__(64 * WPR) void spmm_row_kernel(
     __syncthreads();
     if (w > 0) return;
 #pragma unroll
-    for (int p = 0; p < WPR - 1; ++p) {
+    for (int p = 0; p < WPR - 1; ++p) {  // wave order: deterministic
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[j] += part[p][j][lane];
     }
@@ -1238,6 +1239,8 @@ void pick_row_kernel(SpmmCfg& c, int64_t M, int64_t nnz, int64_t F, int64_t unit
   // against 19.5 for units + combine — so by default only short-row operands take this kernel,
   // with one wave per row (each output a C fmaf chain: the executor folds such a call into the
   // tail that consumes it, gnn_sage_norm_bwd_agg_f32, bit for bit).
+  // (round 5: a dynamic form, one wave per 8 nonzeros of a row up to 16 per workgroup, took the
+  // layer-2 forward to 49 us in the step against 23 for units + combine: not kept)
   if (mode != 1 && avg >= 12.0) return;
   int wpr = avg >= 48.0 ? 8 : (avg >= 12.0 ? 4 : 1);
   if (const char* e = getenv("GNN_SPMM_ROWK_WPR")) {  // experiments
@@ -1599,11 +1602,16 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
                 "gnn_spmm_csr_f32_ex: R (ldr %lld) not aligned for %d-wide vectors", (long long)ldr, c.vw);
     RowFn fn = select_row(c, rmap != nullptr);
     GNN_REQUIRE(fn != nullptr, "gnn_spmm_csr_f32: no row kernel for vw=%d nj=%d wpr=%d", c.vw, c.rnj, c.wpr);
-    if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
-    hipLaunchKernelGGL(fn, dim3((unsigned)(M * c.slices)), dim3(64 * c.wpr), 0, st, rowptr, col, val, (int)M, X, ldx,
-                       Y, ldy, (int)F, c.slices, R, ldr, (const int*)rmap);
+    // timing (gnn_spmm_set_timing_events): the events take the dispatch's own start / end
+    // timestamps (hipExtLaunchKernel), the kernel's duration as rocprofv3 reports it — not an
+    // event pair around the launch, which also brackets the queue's event packets (~7 us each)
+    if (ev0 || ev1)
+      hipExtLaunchKernelGGL(fn, dim3((unsigned)(M * c.slices)), dim3(64 * c.wpr), 0, st, ev0, ev1, 0, rowptr, col, val,
+                            (int)M, X, ldx, Y, ldy, (int)F, c.slices, R, ldr, (const int*)rmap);
+    else
+      hipLaunchKernelGGL(fn, dim3((unsigned)(M * c.slices)), dim3(64 * c.wpr), 0, st, rowptr, col, val, (int)M, X, ldx,
+                         Y, ldy, (int)F, c.slices, R, ldr, (const int*)rmap);
     GNN_LAUNCHED("spmm_row_kernel");
-    if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
     return 0;
   }
   GNN_REQUIRE(c.nunits * c.unit < (int64_t)INT_MAX + c.unit, "gnn_spmm_csr_f32: unit overflow");
@@ -1622,11 +1630,13 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
               "gnn_spmm_csr_f32: grid too large");
   const WorkMap wm = work_map(c, M);
   const dim3 grid((unsigned)(wm.xcd_chunk ? 8 * (int64_t)wm.xcd_chunk : wm.items));
-  if (ev0) GNN_HIP(hipEventRecord(ev0, st), "timing event (start)");
-  hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
-                     (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap, wm);
+  if (ev0 || ev1)  // the dispatch's own start / end timestamps (see the row kernel above)
+    hipExtLaunchKernelGGL(fn, grid, dim3(256), 0, st, ev0, ev1, 0, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
+                          (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap, wm);
+  else
+    hipLaunchKernelGGL(fn, grid, dim3(256), 0, st, rowptr, col, val, (int)M, (int)nnz, (int)c.unit,
+                       (int)c.nunits, X, ldx, Y, ldy, slab, c.ldslab, (int)F, R, ldr, (const int*)rmap, wm);
   GNN_LAUNCHED("spmm_unit_kernel");
-  if (ev1) GNN_HIP(hipEventRecord(ev1, st), "timing event (stop)");
   if (any_split) {
     int crows = combine_rows(M);
     if (const char* e = getenv("GNN_SPMM_CROWS")) crows = std::min(64, std::max(1, atoi(e)));  // A/B
@@ -1635,6 +1645,8 @@ int gnn_spmm_csr_f32_ex(const int32_t* rowptr, const int32_t* col, const float* 
       kern<<<g2, dim3(256), 0, st>>>(rowptr, (int)M, (int)c.unit, slab, c.ldslab, Y, ldy, (int)F, R, ldr,
                                      (const int*)rmap, crows);
     };
+    // (round 5: for the layer-2 forward, every piece of a pass in flight and a row per workgroup
+    // measured equal under the bench — 573.5 / 570.8 vs 574.0 / 570.7 gpu_step: not kept)
     if (c.vw == 4) combine(spmm_combine_kernel<4, COMBINE_LOADS>);
     else if (c.vw == 2) combine(spmm_combine_kernel<2, COMBINE_LOADS>);
     else combine(spmm_combine_kernel<1, COMBINE_LOADS>);

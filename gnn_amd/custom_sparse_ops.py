@@ -36,8 +36,11 @@ import torch
 
 from . import _lib
 
-# Reference module-level timers (custom_sparse_ops.py:11-12). Accumulated in seconds from
-# HIP events when timing is enabled (enable_timing(True)); 0.0 otherwise, as upstream.
+# Reference module-level timers (custom_sparse_ops.py:11-12). Accumulated in seconds from the
+# aggregation kernels' own dispatch timestamps when timing is enabled (enable_timing(True)); 0.0
+# otherwise, as upstream. A backward aggregation the native step executor folds into the layer
+# tail below it (gnn_sage_norm_bwd_agg_f32: the top layer's, when its rows are short) has no
+# launch of its own and is not in spmm_backward_time.
 spmm_forward_time = 0.0
 spmm_backward_time = 0.0
 
@@ -46,7 +49,7 @@ _timing_records: List[Tuple[str, "torch.cuda.Event", "torch.cuda.Event", int]] =
 
 
 def enable_timing(flag: bool = True) -> None:
-    """Record HIP events around every aggregation kernel (main kernel only)."""
+    """Time every aggregation kernel (main kernel only) by its dispatch's start / end timestamps."""
     global _timing_enabled
     _timing_enabled = bool(flag)
 

@@ -87,9 +87,10 @@ int gnn_spmm_kernel_name(int64_t M, int64_t K, int64_t nnz, int64_t F, int64_t l
                          const void* X, const void* Y, int64_t unit_nnz, int residual, char* out,
                          size_t out_bytes);
 
-/* Optional timing hook: when set, the NEXT gnn_spmm_csr_f32 call on this thread records
- * `start` immediately before and `stop` immediately after its main aggregation kernel on
- * the call's stream, then clears the hook. Events are hipEvent_t passed as void*. */
+/* Optional timing hook: when set, the NEXT gnn_spmm_csr_f32 call on this thread launches its
+ * main aggregation kernel with `start` / `stop` as the dispatch's own start and end timestamps
+ * (hipExtLaunchKernel: hipEventElapsedTime(start, stop) = the kernel's duration, as rocprofv3
+ * reports it), then clears the hook. Events are hipEvent_t (created with timing) as void*. */
 void gnn_spmm_set_timing_events(void* start, void* stop);
 
 /* ---------------------------------------------------------------------------------

@@ -14,6 +14,7 @@
 #   cpu1                 bench.py --cpu (BASELINE config 1 on the box's host)
 #   self2                GNN_DIST_BACKEND=gloo bench.py --gpus 2 (self-launched ranks on the one GPU)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS (probes under scripts/)
+#   envpy:ENV:SCRIPT[:ARGS]  the same with ENV (NAME=V;NAME=V)
 set -o pipefail
 TAG=$1
 shift
@@ -73,6 +74,10 @@ EOF
     py)
       script=${arg%%:*}; pargs=""; [ "$script" != "$arg" ] && pargs=${arg#*:}
       timeout -k 10 500 python -u $script $(sp "$pargs") > $out.log 2>&1; rc=$?; tail -5 $out.log ;;
+    envpy)
+      envs=${arg%%:*}; rest=${arg#*:}; script=${rest%%:*}; pargs=""; [ "$script" != "$rest" ] && pargs=${rest#*:}
+      env ${envs//;/ } timeout -k 10 500 python -u $script $(sp "$pargs") > $out.log 2>&1; rc=$?
+      echo "$envs" > $out.env; tail -5 $out.log ;;
     *)
       echo "unknown step $STEP"; rc=2 ;;
   esac

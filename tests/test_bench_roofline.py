@@ -46,7 +46,9 @@ def test_roofline_from_executor_tags_and_positional():
         for tag, li in (("fwd_L0", 0), ("fwd_L1", 1), ("fwd_L2", 2), ("bwd_L1", 1)):
             recs.append(_rec(tag, li, hb, 8, "k_big" if li < 2 else "k_small"))
     roof, detail = bench.roofline_from(recs, batches, A(), None, len(hbs))
-    assert sorted(detail) == ["bwd_L1", "fwd_L0", "fwd_L1", "fwd_L2"]
+    assert sorted(detail) == ["bwd_L1", "bwd_L2", "fwd_L0", "fwd_L1", "fwd_L2"]
+    assert "folded" in detail["bwd_L2"] and "avg_us" not in detail["bwd_L2"]  # listed, not timed
+    assert all("dispatch" in detail[k]["timing"] for k in ("fwd_L0", "bwd_L1"))
     assert roof["kernel"].startswith("k_big") and "over 9 launches" in roof["kernel"]
     # autograd path: five unnamed records per step in call order
     recs = []
@@ -56,3 +58,29 @@ def test_roofline_from_executor_tags_and_positional():
     roof, detail = bench.roofline_from(recs, batches, A(), None, len(hbs))
     assert sorted(detail) == ["bwd_L1", "bwd_L2", "fwd_L0", "fwd_L1", "fwd_L2"]
     assert "over 9 launches" in roof["kernel"]
+
+
+def test_sites_from_trace():
+    """The traced child run's dispatches -> per call site averages (bench.site_trace): steps cut at
+    adam_kernel, aggregation main kernels named in call order, the warm-up steps dropped."""
+    rows, ts = [], 0
+
+    def disp(name, us):
+        nonlocal ts
+        rows.append({"Kernel_Name": f"void (anonymous namespace)::{name}(int const*, float*)",
+                     "Start_Timestamp": str(ts), "End_Timestamp": str(ts + int(us * 1e3))})
+        ts += int(us * 1e3) + 500
+
+    for step in range(5):
+        big = 300.0 if step < 2 else 240.0  # two slow warm-up steps, dropped below
+        disp("spmm_unit_kernel<4, 16, 1, 4, false>", big)
+        disp("spmm_combine_kernel<4, 4>", 10.0)
+        disp("spmm_unit_kernel<4, 16, 1, 4, false>", 200.0)
+        disp("spmm_unit_kernel<4, 64, 1, 16, false>", 16.0 + step)
+        disp("sage_norm_bwd2_kernel<2, true>", 30.0)
+        disp("spmm_unit_kernel<4, 32, 1, 4, true>", 201.0)
+        disp("adam_kernel", 15.0)
+    out = bench.sites_from_trace(rows, 3)
+    assert sorted(out) == ["bwd_L1", "fwd_L0", "fwd_L1", "fwd_L2"]
+    assert out["fwd_L0"] == {"rocprof_avg_us": 240.0, "launches": 3, "kernel": "spmm_unit_kernel<4, 16, 1, 4, false>"}
+    assert out["fwd_L2"]["rocprof_avg_us"] == 19.0 and out["bwd_L1"]["kernel"].endswith("true>")
