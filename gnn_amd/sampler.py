@@ -157,13 +157,15 @@ class DeviceBatch:
     # this batch's GPU extractions (None when no layer was extracted on the GPU)
     err_host: Optional[torch.Tensor] = None
 
-    def check_extraction(self) -> None:
+    def check_extraction(self, err_host: Optional[torch.Tensor] = None) -> None:
         """Raise if a GPU extraction up to and including this batch's saw a device count that
-        disagrees with the host's. The caller makes sure the build stream has passed the flag's
-        copy (StagedX0.wait synchronises on the staging event first)."""
-        if self.err_host is not None and int(self.err_host[0]):
+        disagrees with the host's (``err_host``: the flag of a given build; default the latest).
+        The caller makes sure the build stream has passed the flag's copy (StagedX0.wait
+        synchronises on the staging event first)."""
+        flag = self.err_host if err_host is None else err_host
+        if flag is not None and int(flag[0]):
             raise RuntimeError(f"gnn_ladies_extract_f32: device counts disagree with the host's "
-                               f"(flag {int(self.err_host[0])}); the batch's operand is not used")
+                               f"(flag {int(flag[0])}); the batch's operand is not used")
 
     def tensors(self) -> list:
         """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
@@ -215,8 +217,9 @@ class DeviceBatch:
             # the error flag as it stands after this batch's extractions, into pinned host memory on
             # the same stream: read once the staging event has completed, before the step that
             # consumes the operands is issued (StagedX0.wait)
-            if self.err_host is None:
-                self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            # a flag of its own per build: a rebuilt batch must not overwrite the flag a
+            # staged copy of its previous build is about to read
+            self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self.err_host.copy_(self.graph.err, non_blocking=True)
         return adjs
 

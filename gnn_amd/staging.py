@@ -242,8 +242,10 @@ class StagedX0:
         self._keep = keep
         self.F = F
         self.batch = batch  # the DeviceBatch built on the staging stream, if any
-        # its operands as built by this issue (a later issue may rebuild the same batch)
+        # its operands as built by this issue (a later issue may rebuild the same batch), and the
+        # pinned copy of the extraction error flag taken by this build
         self.adjs = list(batch.adjs) if batch is not None and batch.adjs is not None else None
+        self.err_host = getattr(batch, "err_host", None) if batch is not None else None
 
     def wait(self, retire: Optional["Retirement"] = None) -> torch.Tensor:
         """Make the current stream wait for the staging and return the (n x F) view. The
@@ -251,13 +253,13 @@ class StagedX0:
         each is marked with record_stream (default), or ``retire`` keeps them alive until the
         consuming step has run on the GPU (one event instead of ~40 record_stream calls)."""
         b = self.batch
-        if b is not None and getattr(b, "err_host", None) is not None and _EXTRACT_CHECK == "step":
+        if b is not None and self.err_host is not None and _EXTRACT_CHECK == "step":
             # GPU-extracted layers: their error flag is read before this step is issued, so a
             # device count that disagrees with the host's raises before any kernel consumes the
             # operand (a host wait on the staging event, which the staged work was issued a step
             # ahead of; GNN_EXTRACT_CHECK=end defers the check to DeviceGraph.check at the end)
             self.event.synchronize()
-            b.check_extraction()
+            b.check_extraction(self.err_host)
         cur = torch.cuda.current_stream(self._x0.device)
         cur.wait_event(self.event)
         if retire is None:
