@@ -723,7 +723,9 @@ def _main(args, held):
                              "buffers and found bit-equal to the feature table before the first batch)"}
     stager = staging.Stager(store, exchange)
     torch.manual_seed(0)
-    model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, 0.1, fused=not args.unfused).to(dev)
+    # dropout 0.1 as the reference (main.py:92-96); GNN_BENCH_DROPOUT only for cost measurements
+    dropout = float(os.environ.get("GNN_BENCH_DROPOUT", "0.1"))
+    model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, dropout, fused=not args.unfused).to(dev)
     trainer = Trainer(model, args.lr, dev)
     if args.stage_gate >= 0:
         gate = torch.cuda.Event()
@@ -738,6 +740,8 @@ def _main(args, held):
     # taking CU slots from the layer-0 aggregation they overlap (--compute-priority normal: off).
     lo_pri, hi_pri = torch.cuda.Stream.priority_range()
     compute_stream = torch.cuda.Stream(device=dev, priority=hi_pri) if args.compute_priority == "high" else None
+
+    step_events = [] if os.environ.get("GNN_BENCH_STEP_EVENTS") == "1" else None
 
     def pipeline(next_item, steps, carry=None):
         if compute_stream is None:
@@ -777,6 +781,10 @@ def _main(args, held):
             staged = ahead.popleft()
             x0 = staged.wait(retire)
             db = staged.batch
+            if step_events is not None:  # diagnostics (GNN_BENCH_STEP_EVENTS=1): per-step GPU spans
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+                step_events.append(ev)
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
             # the next batch's staging after this step's launches (its own stream: it still
@@ -789,19 +797,27 @@ def _main(args, held):
                 issued += 1
         return loss
 
-    def timed(fn_):
+    lead_steps = int(os.environ.get("GNN_BENCH_LEAD", "3"))
+
+    def timed(fn_, lead=None):
         """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds).
         Python's cyclic GC is collected before and paused inside the timed region (a gen-2 pass
-        over the process's objects would land in a 33 ms window as a multi-ms stall)."""
+        over the process's objects would land in a 33 ms window as a multi-ms stall). `lead`: a
+        few untimed steps run after the collection, right before the window's synchronize — the
+        collection idles the GPU, and the steps after an idle gap run slow while the chip brings
+        its clock back up (20-step window: 2.01, 1.93, 1.88, 1.82, 1.77 ms ... 1.65 ms from about
+        the 12th step; profiles/round5/window/), so the window starts on a busy chip."""
         import gc
 
         gc.collect()
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-        retire.wait_s = 0.0
         gc.disable()
         try:
+            if lead is not None and lead_steps > 0:
+                lead()
+            if world > 1:
+                torch.distributed.barrier()
+            torch.cuda.synchronize()
+            retire.wait_s = 0.0
             ts = time.perf_counter()
             out = fn_()
             issued = time.perf_counter() - ts - retire.wait_s
@@ -851,8 +867,26 @@ def _main(args, held):
     # (the queue filled during setup holds pre-sampled batches that must not be timed)
     warm = max(args.warmup, loader.prefetch + 2)
     live_ahead = collections.deque()
-    pipeline(nxt_live, warm, live_ahead)
-    e2e_s, e2e_issue, loss = timed(lambda: pipeline(nxt_live, args.steps, live_ahead))
+    pipeline(nxt_live, warm - min(lead_steps, warm), live_ahead)
+    # where the window's time goes: the compute stream's span (first step's first kernel to the last
+    # step's last) beside the wall clock between the two device-wide synchronizations
+    cs = compute_stream if compute_stream is not None else torch.cuda.current_stream(dev)
+    w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def e2e_window():
+        w0.record(cs)
+        out = pipeline(nxt_live, args.steps, live_ahead)
+        w1.record(cs)
+        return out
+
+    e2e_s, e2e_issue, loss = timed(e2e_window, lead=lambda: pipeline(nxt_live, min(lead_steps, warm), live_ahead))
+    if step_events is not None:
+        evs = step_events[-args.steps:] + [w1]
+        log("e2e window step spans (ms): " + " ".join(f"{a.elapsed_time(b):.3f}" for a, b in zip(evs, evs[1:])))
+    window = {"wall_ms": round(1e3 * e2e_s, 3), "compute_stream_ms": round(w0.elapsed_time(w1), 3),
+              "what": "the timed end-to-end window: wall clock between the barrier + synchronize pairs, and the "
+                      "step stream's span over the same steps (the rest: the staging of the batches after the "
+                      "window, which the closing synchronize waits for, and the first launch)"}
     # the batches staged for steps past the window: let their staging finish, then drop them
     torch.cuda.synchronize()
     live_ahead.clear()
@@ -908,6 +942,18 @@ def _main(args, held):
                 lb.plan.peer_meta = f
 
         pipeline(nxt_pre, nwarm)
+
+        def pre_lead():
+            """untimed steps on the warm-up batches right before a timed pass (timed's `lead`)"""
+            was, tm = cso.timing_enabled(), stager.timing
+            cso.enable_timing(False)
+            stager.timing = None  # the lead's uploads are not the timed pass's staging
+            k_[0] = 0
+            pipeline(nxt_pre, min(lead_steps, nwarm))
+            k_[0] = nwarm
+            cso.enable_timing(was)
+            stager.timing = tm
+
         recs = []
         if not args.no_roofline:
             # the aggregation launches timed with HIP events recorded on their stream, over a timed
@@ -915,7 +961,7 @@ def _main(args, held):
             # value comes from a second pass over the same batches without them)
             negotiate_ahead()
             cso.enable_timing(True)
-            timed(lambda: pipeline(nxt_pre, gsteps))
+            timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
             cso.enable_timing(False)
             recs = cso.take_timing_records()
             k_[0] = nwarm
@@ -928,7 +974,7 @@ def _main(args, held):
                 pre[j].host.drop_device()
         stager.timing = []
         negotiate_ahead()
-        step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps))
+        step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
         h_bytes, h_sec = stager.take_timing()
         dp_ab = None
         if world > 1 and getattr(trainer, "bucketed", None) is not None and os.environ.get("GNN_BENCH_DP_AB", "1") == "1":
@@ -945,7 +991,7 @@ def _main(args, held):
                 if native:
                     pre[j].host.drop_device()
             negotiate_ahead()
-            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps))
+            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
             trainer.exchange = trainer.bucketed if first == "bucketed" else None
             dp_ab = {"default": first, first: round(world * gsteps / step_s, 3),
                      ("flat" if first == "bucketed" else "bucketed"): round(world * gsteps / alt_s, 3),
@@ -965,7 +1011,7 @@ def _main(args, held):
                 if native:
                     pre[j].host.drop_device()
             negotiate_ahead()
-            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps))
+            alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
             stager.exchange = exchange
             peer_ab = {"default": args.peer_rows, args.peer_rows: round(world * gsteps / step_s, 3),
                        ("alltoall" if exchange is direct else "direct"): round(world * gsteps / alt_s, 3),
@@ -1080,7 +1126,7 @@ def _main(args, held):
                        "buffer_size": args.buffer_size, "parallelism": f"dp{world}",
                        "peer_rows": (args.peer_rows if world > 1 else None),
                        "nnz_per_batch": int(probe_batch.nnz()), "fused_epilogue": not args.unfused,
-                       "stage_ahead": args.stage_ahead, "stage_gate": args.stage_gate,
+                       "stage_ahead": args.stage_ahead, "stage_gate": args.stage_gate, "dropout": dropout,
                        "locality_sampling": args.locality_sampling, "scale_factor": args.scale_factor,
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
@@ -1092,6 +1138,7 @@ def _main(args, held):
             "dp_exchange_ab": dp_ab,
             "peer_rows_ab": peer_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
+            "e2e_window": window,
             "spmm_per_callsite": spmm_detail,
             "sampler": sampler_cost,
             "feature_staging": staging_info,

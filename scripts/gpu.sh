@@ -8,13 +8,13 @@
 #   tfile:FILE[,FILE]    pytest -m gpu on the named test files only
 #   smoke                __graft_entry__.smoke()
 #   bench[:ARGS]         python bench.py ARGS (',' in ARGS means ' '), JSON line -> bench_TAG_N.json
-#   envbench:ENV:ARGS    bench with ENV (NAME=V;NAME=V) — for A/B/A/B runs of knobs
+#   envbench:ENV:ARGS    bench with ENV (NAME=V+NAME=V) — for A/B/A/B runs of knobs
 #   kstats[:ARGS]        rocprofv3 --kernel-trace --stats of bench.py ARGS -> kstats_TAG_N.csv
 #   ktrace[:ARGS]        rocprofv3 --kernel-trace (per dispatch, trimmed CSV) -> ktrace_TAG_N.csv
 #   cpu1                 bench.py --cpu (BASELINE config 1 on the box's host)
 #   self2                GNN_DIST_BACKEND=gloo bench.py --gpus 2 (self-launched ranks on the one GPU)
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS (probes under scripts/)
-#   envpy:ENV:SCRIPT[:ARGS]  the same with ENV (NAME=V;NAME=V)
+#   envpy:ENV:SCRIPT[:ARGS]  the same with ENV (NAME=V+NAME=V)
 set -o pipefail
 TAG=$1
 shift
@@ -46,7 +46,7 @@ for STEP in "$@"; do
       python3 -c "import json;d=json.loads(open('$out.json').read().strip().splitlines()[-1]);print('value',d['value'],'gpu_step',(d.get('gpu_step') or {}).get('value'))" 2>/dev/null ;;
     envbench)
       envs=${arg%%:*}; bargs=""; [ "$envs" != "$arg" ] && bargs=${arg#*:}
-      env ${envs//;/ } timeout -k 10 500 python -u bench.py $(sp "$bargs") > $out.json 2> $out.err; rc=$?
+      env ${envs//+/ } timeout -k 10 500 python -u bench.py $(sp "$bargs") > $out.json 2> $out.err; rc=$?
       echo "$envs" > $out.env
       python3 -c "import json;d=json.loads(open('$out.json').read().strip().splitlines()[-1]);print('$envs','value',d['value'],'gpu_step',(d.get('gpu_step') or {}).get('value'))" 2>/dev/null ;;
     kstats|ktrace)
@@ -76,7 +76,7 @@ EOF
       timeout -k 10 500 python -u $script $(sp "$pargs") > $out.log 2>&1; rc=$?; tail -5 $out.log ;;
     envpy)
       envs=${arg%%:*}; rest=${arg#*:}; script=${rest%%:*}; pargs=""; [ "$script" != "$rest" ] && pargs=${rest#*:}
-      env ${envs//;/ } timeout -k 10 500 python -u $script $(sp "$pargs") > $out.log 2>&1; rc=$?
+      env ${envs//+/ } timeout -k 10 500 python -u $script $(sp "$pargs") > $out.log 2>&1; rc=$?
       echo "$envs" > $out.env; tail -5 $out.log ;;
     *)
       echo "unknown step $STEP"; rc=2 ;;
