@@ -399,22 +399,23 @@ template <bool KMAJ>
 __device__ __forceinline__ void s3_store(unsigned short* __restrict__ S, int t, const float v[8]) {
   const int rr = KMAJ ? (t & 127) : (t >> 1);
   const int kh = KMAJ ? (t >> 7) : (t & 1);
-  // per pair of elements: 4 v_and, the two subtractions on packed fp32 (v_pk_add_f32 where the
-  // compiler pairs them) and 3 v_perm (one per piece, packing the two high halves): 159 VALU
-  // per two k tiles in the main loop against 214 for the element-wise form (and + or_sdwa +
-  // lshr + and_or + moves). The kernel is bound by the SIMD's issue port (VALU + MFMA issue).
+  // per pair of elements: 4 v_and, 4 v_sub_f32 and 3 v_perm (one per piece, packing the two high
+  // halves). The kernel is bound by the SIMD's issue port (VALU + MFMA issue); the subtractions
+  // stay scalar: the packed form (v_pk_add_f32, two elements per instruction) measured 2-5 %
+  // slower on every layer pair (profiles/round5/gemm_split/), the element-wise and/or form
+  // (and + or_sdwa + lshr + and_or + moves, 214 VALU per two k tiles) slower still.
   u4v ph, pm, pl;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const f2 x = f2{v[2 * j], v[2 * j + 1]};
-    const unsigned int h0 = __float_as_uint(x.x) & 0xffff0000u, h1 = __float_as_uint(x.y) & 0xffff0000u;
-    const f2 r = x - f2{__uint_as_float(h0), __uint_as_float(h1)};  // exact
-    const unsigned int m0 = __float_as_uint(r.x) & 0xffff0000u, m1 = __float_as_uint(r.y) & 0xffff0000u;
-    const f2 l = r - f2{__uint_as_float(m0), __uint_as_float(m1)};  // exact, <= 8 significant bits
+    const float x0 = v[2 * j], x1 = v[2 * j + 1];
+    const unsigned int h0 = __float_as_uint(x0) & 0xffff0000u, h1 = __float_as_uint(x1) & 0xffff0000u;
+    const float r0 = x0 - __uint_as_float(h0), r1 = x1 - __uint_as_float(h1);  // exact
+    const unsigned int m0 = __float_as_uint(r0) & 0xffff0000u, m1 = __float_as_uint(r1) & 0xffff0000u;
+    const float l0 = r0 - __uint_as_float(m0), l1 = r1 - __uint_as_float(m1);  // exact, <= 8 significant bits
     // bytes {lo.2, lo.3, hi.2, hi.3}: the bf16 (high half) of element 2j low, of 2j+1 high
     ph[j] = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
     pm[j] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
-    pl[j] = __builtin_amdgcn_perm(__float_as_uint(l.y), __float_as_uint(l.x), 0x07060302u);
+    pl[j] = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
   }
   const int off = s3_chunk<KMAJ>(rr, kh);
   *reinterpret_cast<u4v*>(S + off) = ph;
