@@ -752,6 +752,15 @@ def _main(args, held):
         torch.cuda.current_stream(dev).wait_stream(compute_stream)
         return loss
 
+    def next_batch(ahead):
+        """The batch after the current one, for the trainer's layer-0 prefetch during the gradient
+        all-reduce (N > 1): already staged (its staging was issued a step or more ago)."""
+        if not ahead:
+            return None
+        nb = ahead[0]
+        x0n = nb.wait(retire)
+        return x0n, nb.adjs, nb.batch.sampled_nodes, nb.batch.labels
+
     def _pipeline(next_item, steps, carry=None):
         """next_item() -> (StagePlan, batch_fn); batch_fn() makes the DeviceBatch (H2D when
         needed + the operand builds). The X0 staging and batch_fn of batches i+1 .. i+A (A =
@@ -785,7 +794,8 @@ def _main(args, held):
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
                 step_events.append(ev)
-            loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels)
+            loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels,
+                                prefetch=(lambda: next_batch(ahead)) if world > 1 else None)
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
             # the next batch's staging after this step's launches (its own stream: it still
             # overlaps this step, behind --stage-gate's event when set), so a timed pass's first
@@ -893,7 +903,7 @@ def _main(args, held):
     log(f"end to end: {world * args.steps / e2e_s:.1f} mini-batches/s ({time.time() - t0:.1f}s)")
 
     # ------------------------------------------------- GPU step over distinct pre-sampled batches
-    gpu_step, roof, spmm_detail, staging_info, dp_ab, peer_ab = None, None, {}, None, None, None
+    gpu_step, roof, spmm_detail, staging_info, dp_ab, peer_ab, prefetch_ab = None, None, {}, None, None, None, None
     step_batches = []
     if not args.no_gpu_step:
         nwarm = max(2, min(args.warmup, 10))
@@ -998,6 +1008,32 @@ def _main(args, held):
                      "what": "gpu_step mini-batches/s over the same pre-sampled batches with each gradient "
                              "exchange (bucketed: all-to-all per backward stage overlapped with the backward, "
                              "then the clip factors, shard sums and one gather; flat: clip + one all-reduce)"}
+        prefetch_ab = None
+        if world > 1 and trainer.exchange is None and os.environ.get("GNN_BENCH_PREFETCH_AB", "1") == "1":
+            # the step without the next batch's layer-0 aggregation issued during the all-reduce
+            # (GNN_PREFETCH_L0=0), over the same batches, after the reported passes
+            k_[0] = nwarm
+            torch.cuda.synchronize()
+            for j in range(len(dbs)):
+                dbs[j] = None
+                if native:
+                    pre[j].host.drop_device()
+            negotiate_ahead()
+            was = os.environ.get("GNN_PREFETCH_L0")
+            os.environ["GNN_PREFETCH_L0"] = "0" if was != "0" else "1"
+            try:
+                alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
+            finally:
+                if was is None:
+                    os.environ.pop("GNN_PREFETCH_L0", None)
+                else:
+                    os.environ["GNN_PREFETCH_L0"] = was
+            on = was != "0"
+            prefetch_ab = {"default": "on" if on else "off", ("on" if on else "off"): round(world * gsteps / step_s, 3),
+                           ("off" if on else "on"): round(world * gsteps / alt_s, 3),
+                           "what": "gpu_step mini-batches/s over the same pre-sampled batches with and without the next "
+                                   "batch's layer-0 aggregation issued while the gradient all-reduce runs "
+                                   "(GNN_PREFETCH_L0; the flat exchange)"}
         peer_ab = None
         if world > 1 and direct is not None and os.environ.get("GNN_BENCH_PEER_AB", "1") == "1":
             # the other peer-row form over the same batches (direct reads of the IPC-mapped peer
@@ -1136,6 +1172,7 @@ def _main(args, held):
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,
             "dp_exchange_ab": dp_ab,
+            "prefetch_l0_ab": prefetch_ab,
             "peer_rows_ab": peer_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "e2e_window": window,

@@ -416,6 +416,21 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_HIP(hipEventRecord((hipEvent_t)d[GNN_SH_STAGE_EVENT], st), "hipEventRecord (stage gate)");
     return 0;
   };
+  // phase (GNN_SH_PHASE): 1 = only layer 0's forward aggregation, into this workspace (a data-
+  // parallel caller issues the next batch's while the gradient all-reduce runs); 2 = the step with
+  // that aggregation already issued into this workspace by a phase-1 call (same descriptor plan)
+  const int64_t phase = d[GNN_SH_PHASE];
+  GNN_REQUIRE(phase >= 0 && phase <= 2, "gnn_train_step: phase %lld", (long long)phase);
+  auto first_agg = [&]() -> int {
+    const LayerBufs& b = pl.lb[0];
+    return gnn_spmm_csr_f32(P<const int32_t>(d, 0, GNN_SL_ROWPTR), P<const int32_t>(d, 0, GNN_SL_COL),
+                            P<const float>(d, 0, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                            b.ws_fwd, b.b_fwd, 0, st);
+  };
+  if (phase == 1) {
+    GNN_TRY(first_agg());
+    return stage_gate(0);
+  }
   // ------------------------------------------------------------------ forward
   for (int l = 0; l < pl.nl; ++l) {
     LayerBufs& b = pl.lb[l];
@@ -440,11 +455,13 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       float* Cb[1] = {b.hB};
       GNN_TRY(gnn::gemm_split3_as_batch(0, 0, b.M, N, b.F, 1, 2, 0, Ab, b.ldo, Bb, b.F, Cb, N, b.ws_gemm_f2, b.b_gemm_f,
                                         aux->s));
-      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
-      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
-                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
-                               b.ws_fwd, b.b_fwd, 0, st));
-      GNN_TRY(stage_gate(l));
+      if (phase != 2 || l != 0) {
+        arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+        GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                                 P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                                 b.ws_fwd, b.b_fwd, 0, st));
+        GNN_TRY(stage_gate(l));
+      }
       const float* Aw[1] = {b.feat};
       const float* Bw[1] = {WW};
       float* Cw[1] = {b.hW};
@@ -456,19 +473,23 @@ int gnn_train_step_f32(const int64_t* d, void* workspace, size_t workspace_bytes
       GNN_TRY(gnn_gather_rows_f32(b.X, b.ldx, P<const int64_t>(d, l, GNN_SL_SAMPLED), b.xs, b.ldo, nullptr, b.M,
                                   b.F, aux->s));
       GNN_TRY(mm_xwt(ha, b.xs, b.ldo, WB, b.F, b.hB, N, b.M, N, b.F));
-      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
-      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
-                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
-                               b.ws_fwd, b.b_fwd, 0, st));
-      GNN_TRY(stage_gate(l));
+      if (phase != 2 || l != 0) {
+        arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+        GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                                 P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                                 b.ws_fwd, b.b_fwd, 0, st));
+        GNN_TRY(stage_gate(l));
+      }
       GNN_TRY(mm_xwt(h, b.feat, b.ldo, WW, b.F, b.hW, N, b.M, N, b.F));
       GNN_TRY(fork_join(aux, aux->s, st));  // the tail reads hB
     } else {
-      arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
-      GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
-                               P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
-                               b.ws_fwd, b.b_fwd, 0, st));
-      GNN_TRY(stage_gate(l));
+      if (phase != 2 || l != 0) {
+        arm(0, l, b.M, b.K, b.nnz, b.F, b.Fk, b.ldx, b.ldo, b.X, b.feat, 0);
+        GNN_TRY(gnn_spmm_csr_f32(P<const int32_t>(d, l, GNN_SL_ROWPTR), P<const int32_t>(d, l, GNN_SL_COL),
+                                 P<const float>(d, l, GNN_SL_VAL), b.M, b.K, b.nnz, b.X, b.ldx, b.feat, b.ldo, b.Fk,
+                                 b.ws_fwd, b.b_fwd, 0, st));
+        GNN_TRY(stage_gate(l));
+      }
       // x[sampled] feeds only linearB and its weight gradient: when both run on split3 (and X's
       // rows have the aggregation output's stride) the GEMMs read X's rows through the index
       // instead of a gathered copy (bit-identical operands)

@@ -25,7 +25,7 @@ from . import custom_sparse_ops as cso
 VERSION, MAX_LAYERS, HEADER, LAYER_SLOTS, SAGE, GCN = 1, 4, 24, 32, 0, 1
 (H_VERSION, H_LAYERS, H_KIND, H_X0, H_LDX0, H_F0, H_HEAD_W, H_HEAD_B, H_HEAD_GW, H_HEAD_GB, H_CLASSES, H_LABELS,
  H_LDL, H_HEAD_SEED, H_PDROP_BITS, H_TRAINING, H_LOSS, H_NHID, H_TIMING, H_GRAD_EVENTS, H_STAGE_EVENT,
- H_STAGE_LAYER) = range(22)
+ H_STAGE_LAYER, H_PHASE) = range(23)
 TIMING_SLOTS = 16
 (L_ROWPTR, L_COL, L_VAL, L_M, L_K, L_NNZ, L_TROWPTR, L_TCOL, L_TVAL, L_SAMPLED, L_NSAMPLED, L_RMAP, L_WW, L_BW,
  L_WB, L_BB, L_SCALE, L_OFFSET, L_GWW, L_GBW, L_GWB, L_GBB, L_GSCALE, L_GOFFSET, L_SEED) = range(25)
@@ -135,11 +135,91 @@ class NativeStep:
             stages.append([i for i, p in enumerate(self.params) if id(p) in mine])
         return stages
 
+    @staticmethod
+    def _batch_key(x0, adjs, labels):
+        return (x0.data_ptr(), tuple(x0.shape), x0.stride(0), labels.data_ptr(), tuple(id(op) for op in adjs))
+
+    def prefetch(self, x0, adjs, sampled_nodes, labels, stage_gate=None) -> None:
+        """Issue ONLY this batch's layer-0 forward aggregation A_0·x0 (GNN_SH_PHASE 1) into a
+        workspace kept for its step, on the current stream; the next ``step`` on the same batch
+        (same x0, operands and labels) runs without issuing it again (phase 2). It reads only the
+        batch, never a parameter, so a data-parallel trainer issues it between the gradient
+        all-reduce's launch and the optimizer step: it runs while the all-reduce does (reference:
+        main.py:122-168, where the next batch's forward starts after the exchange and the step).
+        No dropout seed is drawn here: the step draws them, in the same order as without it."""
+        d = self._desc(x0, adjs, sampled_nodes, labels, seeds=False)
+        if stage_gate is not None and int(stage_gate[1]) == 0:
+            self._set_gate(d, stage_gate)
+        d[H_PHASE] = 1
+        ws, wsb = self._workspace(d, x0.device)
+        L = _lib.lib()
+        with _lib.on_device(x0.device):
+            _lib.check(L.gnn_train_step_f32(d.ctypes.data, ws.data_ptr(), wsb, _lib.stream_of(x0.device)),
+                       "gnn_train_step_f32 (phase 1)")
+        # the batch's tensors and operands are held with the key, so no other batch can take
+        # their addresses or ids while the prefetched aggregation waits for its step
+        self._pre = (self._batch_key(x0, adjs, labels), ws, wsb, (x0, tuple(adjs), labels))
+
+    def drop_prefetch(self) -> None:
+        self._pre = None
+
+    @staticmethod
+    def _set_gate(d, stage_gate):
+        ev, layer = stage_gate
+        if not getattr(ev, "_gnn_created", False):
+            ev.record()  # creates the underlying hipEvent once; the step re-records it
+            ev._gnn_created = True
+        d[H_STAGE_EVENT], d[H_STAGE_LAYER] = ev.cuda_event, int(layer)
+
+    @staticmethod
+    def _workspace(d, device):
+        wsb = _lib.lib().gnn_train_step_workspace_bytes(d.ctypes.data)
+        if wsb == 0:
+            raise RuntimeError("gnn_train_step_workspace_bytes: " + _lib.lib().gnn_last_error().decode(errors="replace"))
+        return torch.empty(wsb, dtype=torch.uint8, device=device), wsb
+
     def step(self, x0, adjs, sampled_nodes, labels, grad_events=None, stage_gate=None) -> torch.Tensor:
         """grad_events: optional [head event, layer 0 event, layer 1 event, ...] (torch.cuda.Event)
         recorded on the step's stream once those gradients are final (GNN_SH_GRAD_EVENTS).
         stage_gate: optional (torch.cuda.Event, layer): the event is recorded right after that
-        layer's forward aggregation (GNN_SH_STAGE_EVENT; staging.Stager waits on it)."""
+        layer's forward aggregation (GNN_SH_STAGE_EVENT; staging.Stager waits on it).
+        A ``prefetch`` of this same batch (the last one issued) supplies the layer-0 aggregation."""
+        d = self._desc(x0, adjs, sampled_nodes, labels, seeds=True)
+        pre, self._pre = getattr(self, "_pre", None), None
+        if pre is not None and pre[0] == self._batch_key(x0, adjs, labels):
+            d[H_PHASE] = 2
+            ws, wsb = pre[1], pre[2]
+            if stage_gate is not None and int(stage_gate[1]) == 0:
+                stage_gate = None  # recorded by the prefetch, after the layer-0 aggregation
+        else:
+            ws, wsb = None, 0
+        loss = torch.empty((), dtype=torch.float32, device=x0.device)
+        d[H_LOSS] = loss.data_ptr()
+        timing = self._arm_timing(d, len(adjs)) if cso.timing_enabled() else None
+        E = None
+        if grad_events is not None:
+            E = np.zeros(1 + len(grad_events), dtype=np.int64)
+            E[0] = len(E)
+            for i, ev in enumerate(grad_events):
+                if ev is not None:
+                    ev.record()  # creates the underlying hipEvent; the step re-records it
+                    E[1 + i] = ev.cuda_event
+            d[H_GRAD_EVENTS] = E.ctypes.data
+        if stage_gate is not None:
+            self._set_gate(d, stage_gate)
+        L = _lib.lib()
+        dp = d.ctypes.data
+        if ws is None:
+            ws, wsb = self._workspace(d, x0.device)
+        with _lib.on_device(x0.device):
+            _lib.check(L.gnn_train_step_f32(dp, ws.data_ptr(), wsb, _lib.stream_of(x0.device)), "gnn_train_step_f32")
+        if timing is not None:
+            self._collect_timing(*timing)
+        for p, gr in zip(self.params, self.grads):
+            p.grad = gr
+        return loss
+
+    def _desc(self, x0, adjs, sampled_nodes, labels, seeds: bool):
         model = self.model
         training = model.training
         tr = bool(training and self.p_enc > 0)
@@ -160,39 +240,9 @@ class NativeStep:
                 r = getattr(s, "_gnn_rmap", None)
                 d[b + L_RMAP] = _p(r) if li >= 1 else 0
             # the Python path draws one seed per layer tail, then one for the head (fused.py)
-            d[b + L_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if tr else 0
-        d[H_HEAD_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if tr else 0
-        loss = torch.empty((), dtype=torch.float32, device=x0.device)
-        d[H_LOSS] = loss.data_ptr()
-        timing = self._arm_timing(d, len(adjs)) if cso.timing_enabled() else None
-        E = None
-        if grad_events is not None:
-            E = np.zeros(1 + len(grad_events), dtype=np.int64)
-            E[0] = len(E)
-            for i, ev in enumerate(grad_events):
-                if ev is not None:
-                    ev.record()  # creates the underlying hipEvent; the step re-records it
-                    E[1 + i] = ev.cuda_event
-            d[H_GRAD_EVENTS] = E.ctypes.data
-        if stage_gate is not None:
-            ev, layer = stage_gate
-            if not getattr(ev, "_gnn_created", False):
-                ev.record()  # creates the underlying hipEvent once; the step re-records it
-                ev._gnn_created = True
-            d[H_STAGE_EVENT], d[H_STAGE_LAYER] = ev.cuda_event, int(layer)
-        L = _lib.lib()
-        dp = d.ctypes.data
-        wsb = L.gnn_train_step_workspace_bytes(dp)
-        if wsb == 0:
-            raise RuntimeError("gnn_train_step_workspace_bytes: " + L.gnn_last_error().decode(errors="replace"))
-        ws = torch.empty(wsb, dtype=torch.uint8, device=x0.device)
-        with _lib.on_device(x0.device):
-            _lib.check(L.gnn_train_step_f32(dp, ws.data_ptr(), wsb, _lib.stream_of(x0.device)), "gnn_train_step_f32")
-        if timing is not None:
-            self._collect_timing(*timing)
-        for p, gr in zip(self.params, self.grads):
-            p.grad = gr
-        return loss
+            d[b + L_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if (tr and seeds) else 0
+        d[H_HEAD_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if (tr and seeds) else 0
+        return d
 
     @staticmethod
     def _arm_timing(d, nl):

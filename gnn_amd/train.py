@@ -128,7 +128,26 @@ class Trainer:
             p.grad = g
         return flat
 
-    def step(self, x0, adjs, sampled_nodes, labels) -> torch.Tensor:
+    def _next_batch(self, prefetch):
+        """The next batch (x0, adjs, sampled_nodes, labels) for the executor's layer-0 prefetch, or
+        None: data-parallel runs only (there the all-reduce leaves the compute stream idle), the
+        flat exchange, not while the per-aggregation timing runs, GNN_PREFETCH_L0=0 turns it off."""
+        if prefetch is None or self.executor is None or os.environ.get("GNN_PREFETCH_L0", "1") == "0":
+            return None
+        from . import custom_sparse_ops as cso
+
+        if cso.timing_enabled():
+            return None
+        nxt = prefetch() if callable(prefetch) else prefetch
+        if nxt is None or not self.executor.supports(*nxt):
+            return None
+        return nxt
+
+    def step(self, x0, adjs, sampled_nodes, labels, prefetch=None) -> torch.Tensor:
+        """One training step. ``prefetch``: the next batch (x0, adjs, sampled_nodes, labels), or a
+        callable returning it, whose layer-0 forward aggregation a data-parallel run issues while
+        this step's gradient all-reduce is in flight (gnn_amd.executor.NativeStep.prefetch; the
+        next step then skips it). Results are the same with or without it."""
         if not self.model.training:  # module.train() walks every submodule: ~50 µs of host time
             self.model.train()
         if self.executor is not None and self.executor.supports(x0, adjs, sampled_nodes, labels):
@@ -143,7 +162,17 @@ class Trainer:
                                       stage_gate=self.stage_gate)
             if self.dp:
                 flat = self.optimizer.clip_to_flat()
-                torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
+                nxt = self._next_batch(prefetch)
+                if nxt is not None:
+                    # the all-reduce runs on the collective's stream; the next batch's layer-0
+                    # aggregation (no parameter in it) fills the compute stream meanwhile, and the
+                    # optimizer step waits for the sum (Work.wait: a stream wait, not a host one)
+                    work = torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group,
+                                                        async_op=True)
+                    self.executor.prefetch(*nxt, stage_gate=self.stage_gate)
+                    work.wait()
+                else:
+                    torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
                 self.optimizer.step(clipped=True)
             else:
                 self.optimizer.step()

@@ -31,7 +31,12 @@
  *     step's stream right after layer GNN_SH_STAGE_LAYER's forward aggregation — the caller's
  *     staging stream waits on it before the next batches' row gathers and layer extractions, so
  *     those gather-bound kernels run beside the GEMMs and tails instead of competing with the
- *     aggregation for L2 (main.py:129-137's staging, overlapped with the step).
+ *     aggregation for L2 (main.py:129-137's staging, overlapped with the step);
+ *     and the phase (GNN_SH_PHASE): 0 = the whole step; 1 = only layer 0's forward aggregation
+ *     A_0·x0, into the workspace (a data-parallel caller issues the NEXT batch's while this
+ *     step's gradient all-reduce runs: it reads only the batch, never a parameter); 2 = the step
+ *     of a batch whose layer-0 aggregation a phase-1 call with the same descriptor already issued
+ *     into the same workspace (it is not issued again). 0 and 1 + 2 give the same results.
  *   layer l: the operand A (rowptr / col / val, M x K, nnz) and its transpose (K x M, layers >= 1),
  *     sampled (int64 [M], SAGE) and rmap (int32 [K], rmap[sampled[i]] = i, SAGE layers >= 1),
  *     weights W_W / W_B (N x F row-major), biases, scale / offset, their gradient buffers, the
@@ -60,7 +65,7 @@ enum {
   GNN_SH_HEAD_W = 6, GNN_SH_HEAD_B = 7, GNN_SH_HEAD_GW = 8, GNN_SH_HEAD_GB = 9, GNN_SH_CLASSES = 10,
   GNN_SH_LABELS = 11, GNN_SH_LDL = 12, GNN_SH_HEAD_SEED = 13, GNN_SH_PDROP_BITS = 14, GNN_SH_TRAINING = 15,
   GNN_SH_LOSS = 16, GNN_SH_NHID = 17, GNN_SH_TIMING = 18, GNN_SH_GRAD_EVENTS = 19, GNN_SH_STAGE_EVENT = 20,
-  GNN_SH_STAGE_LAYER = 21
+  GNN_SH_STAGE_LAYER = 21, GNN_SH_PHASE = 22
 };
 enum {
   GNN_SL_ROWPTR = 0, GNN_SL_COL = 1, GNN_SL_VAL = 2, GNN_SL_M = 3, GNN_SL_K = 4, GNN_SL_NNZ = 5,

@@ -124,7 +124,7 @@ def _native_model(seed, F, ncls, fused):
     return build_model("graphsage", F, 32, [1, 1, 1], ncls, dropout=0.0, fused=fused)
 
 
-def _native_trainer_worker(rank, world, port, q, buckets=True):
+def _native_trainer_worker(rank, world, port, q, buckets=True, prefetch=False):
     """The benchmark's N > 1 branch: the executor step, then (buckets=True, GNN_DP_BUCKETS=1) the
     bucketed exchange overlapped with the backward (gnn_amd.dp) or (buckets=False, the default)
     ClipAdam.clip_to_flat -> all_reduce(SUM); then Adam (train.py, Trainer.step)."""
@@ -149,8 +149,16 @@ def _native_trainer_worker(rank, world, port, q, buckets=True):
         assert tr.executor is not None and tr.executor.supports(x0, db.adjs, db.sampled_nodes, db.labels), \
             "the executor branch must be the one exercised"
         assert (tr.exchange is not None) == buckets, "the exchange variant under test must be the one in use"
-        losses = [float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels)) for _ in range(2)]
+        losses, taken = [], []
+        for s in range(2):
+            # prefetch: the batch of the next step (the same one here) — its layer-0 aggregation
+            # issued while this step's all-reduce runs, then not issued again by the next step
+            nxt = (x0, db.adjs, db.sampled_nodes, db.labels) if prefetch and s == 0 else None
+            losses.append(float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels, prefetch=nxt)))
+            taken.append(getattr(tr.executor, "_pre", None) is not None)
         torch.cuda.synchronize()
+        if taken != [prefetch, False]:
+            raise AssertionError(f"prefetch taken {taken}")
         q.put((rank, "ok", losses, [p.detach().cpu().numpy().copy() for p in net.parameters()]))
     except Exception as e:
         q.put((rank, f"error: {e!r}", None, None))
@@ -222,6 +230,22 @@ def test_trainer_executor_dp_step_matches_reference(buckets):
             sure &= np.abs(gg) > 1e-4 * max(np.abs(gg).max(), 1e-12)
         assert sure.mean() > 0.5
         np.testing.assert_allclose(got[sure], want[sure], rtol=1e-4, atol=1e-6, err_msg=f"param {i}")
+
+
+def test_dp_layer0_prefetch_is_bit_identical():
+    """The flat data-parallel step with the next batch's layer-0 aggregation issued while the
+    all-reduce runs (Trainer.step(prefetch=...), the bench's N > 1 default) against the same two
+    steps without it: losses and parameters bit for bit on both ranks."""
+    outs = {}
+    for pf in (False, True):
+        out = _spawn(_native_trainer_worker, extra=(False, pf))
+        for rank, status, _, _ in out:
+            assert status == "ok", f"prefetch={pf} rank {rank}: {status}"
+        outs[pf] = out
+    for rank in range(2):
+        assert outs[True][rank][2] == outs[False][rank][2], rank
+        for a, b in zip(outs[True][rank][3], outs[False][rank][3]):
+            assert np.array_equal(a, b), rank
 
 
 def _exchange_worker(rank, world, port, q):

@@ -195,3 +195,35 @@ def test_stream_overlap_variants_are_bit_identical(dev, monkeypatch):
         for s in range(2):
             for i, (x, y) in enumerate(zip(g[s], g0[s])):
                 assert torch.equal(x, y), ("gradient differs", v, s, i)
+
+
+def test_layer0_prefetch_is_bit_identical(dev):
+    """NativeStep.prefetch (GNN_SH_PHASE 1: only the layer-0 forward aggregation, issued ahead
+    into the step's workspace) followed by the step on the same batch (phase 2: not issued again)
+    against the plain step: loss and every gradient bit for bit over two Adam steps. A prefetch of
+    another batch is not taken by the step (the key names the batch), and a step draws the same
+    dropout seeds with or without one."""
+    model_name, F, ncls, db, x0 = _batch("reddit_sage", dev)
+    res = []
+    for mode in ("plain", "prefetch", "other"):
+        tr = _trainer(model_name, F, ncls, dev, native=True)
+        losses, grads = [], []
+        for it in range(2):
+            torch.manual_seed(100 + it)
+            if mode == "prefetch":
+                tr.executor.prefetch(x0, db.adjs, db.sampled_nodes, db.labels)
+                assert tr.executor._pre is not None
+            elif mode == "other":
+                # same data, another view object of x0 and a copy of the labels: another batch
+                tr.executor.prefetch(x0, db.adjs, db.sampled_nodes, db.labels.clone())
+            losses.append(float(tr.step(x0, db.adjs, db.sampled_nodes, db.labels)))
+            assert tr.executor._pre is None
+            grads.append([p.grad.detach().clone() for p in tr.params])
+        torch.cuda.synchronize()
+        res.append((losses, grads))
+    l0, g0 = res[0]
+    for mode, (l, g) in zip(("prefetch", "other"), res[1:]):
+        assert l == l0, (mode, l, l0)
+        for s in range(2):
+            for i, (x, y) in enumerate(zip(g[s], g0[s])):
+                assert torch.equal(x, y), ("gradient differs", mode, s, i)
