@@ -175,6 +175,9 @@ class Trainer:
                     torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
                 self.optimizer.step(clipped=True)
             else:
+                # N = 1 takes no prefetch: issuing it with the clip + Adam kernels moved to a side
+                # stream beside it measured 0.5-0.8 % slower (two cross-stream events per step
+                # against ~30 us of small launches; profiles/round5/prefetch_l0/)
                 self.optimizer.step()
             return loss
         for p in self.params:
