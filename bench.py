@@ -786,17 +786,22 @@ def _main(args, held):
         while not persistent and issued < min(max(1, args.stage_ahead) + 1, steps):
             ahead.append(stager.issue(*next_item()))
             issued += 1
+        ph = host_phases
         for i in range(steps):
+            t0_ = time.perf_counter()
             staged = ahead.popleft()
             x0 = staged.wait(retire)
             db = staged.batch
+            t1_ = time.perf_counter()
             if step_events is not None:  # diagnostics (GNN_BENCH_STEP_EVENTS=1): per-step GPU spans
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
                 step_events.append(ev)
             loss = trainer.step(x0, staged.adjs, db.sampled_nodes, db.labels,
                                 prefetch=(lambda: next_batch(ahead)) if world > 1 else None)
+            t2_ = time.perf_counter()
             retire.retire(staged)  # held until the step has run (no per-tensor record_stream)
+            t3_ = time.perf_counter()
             # the next batch's staging after this step's launches (its own stream: it still
             # overlaps this step, behind --stage-gate's event when set), so a timed pass's first
             # kernels start without waiting for it
@@ -805,9 +810,17 @@ def _main(args, held):
             elif issued < steps:
                 ahead.append(stager.issue(*next_item()))
                 issued += 1
+            t4_ = time.perf_counter()
+            ph[0] += t1_ - t0_
+            ph[1] += t2_ - t1_
+            ph[2] += t3_ - t2_
+            ph[3] += t4_ - t3_
         return loss
 
     lead_steps = int(os.environ.get("GNN_BENCH_LEAD", "3"))
+    # host wall time per pipeline phase (staged-batch wait, step issue, retire, next staging issue),
+    # accumulated by _pipeline and reset by timed(): where the issuing thread's time goes
+    host_phases = [0.0, 0.0, 0.0, 0.0]
 
     def timed(fn_, lead=None):
         """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds).
@@ -828,9 +841,14 @@ def _main(args, held):
                 torch.distributed.barrier()
             torch.cuda.synchronize()
             retire.wait_s = 0.0
+            host_phases[:] = [0.0, 0.0, 0.0, 0.0]
             ts = time.perf_counter()
+            cpu0 = time.thread_time()
             out = fn_()
             issued = time.perf_counter() - ts - retire.wait_s
+            # the issuing thread's CPU time (HIP's blocking waits may spin: an upper bound)
+            timed.cpu_s = time.thread_time() - cpu0
+            timed.phases = list(host_phases)
             torch.cuda.synchronize()
             if world > 1:
                 torch.distributed.barrier()
@@ -890,6 +908,7 @@ def _main(args, held):
         return out
 
     e2e_s, e2e_issue, loss = timed(e2e_window, lead=lambda: pipeline(nxt_live, min(lead_steps, warm), live_ahead))
+    e2e_cpu, e2e_phases = timed.cpu_s, timed.phases
     if step_events is not None:
         evs = step_events[-args.steps:] + [w1]
         log("e2e window step spans (ms): " + " ".join(f"{a.elapsed_time(b):.3f}" for a, b in zip(evs, evs[1:])))
@@ -985,6 +1004,7 @@ def _main(args, held):
         stager.timing = []
         negotiate_ahead()
         step_s, step_issue, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
+        step_cpu = timed.cpu_s
         h_bytes, h_sec = stager.take_timing()
         dp_ab = None
         if world > 1 and getattr(trainer, "bucketed", None) is not None and os.environ.get("GNN_BENCH_DP_AB", "1") == "1":
@@ -1057,6 +1077,7 @@ def _main(args, held):
         gpu_step = {"value": round(world * gsteps / step_s, 3), "unit": "mini-batches/s",
                     "ms_per_step": round(1e3 * step_s / gsteps, 3),
                     "host_issue_ms_per_step": round(1e3 * step_issue / gsteps, 3),
+                    "host_cpu_ms_per_step": round(1e3 * step_cpu / gsteps, 3),
                     "what": f"{gsteps} distinct pre-sampled batches per rank (none cycled); "
                             + ("each batch's blob upload (one H2D), X0 staging, GPU layer extraction / operand builds "
                                "and the whole training step inside the timed region" if native else
@@ -1175,6 +1196,9 @@ def _main(args, held):
             "prefetch_l0_ab": prefetch_ab,
             "peer_rows_ab": peer_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
+            "host_cpu_ms_per_step_e2e": round(1e3 * e2e_cpu / args.steps, 3),
+            "host_phases_ms_per_step_e2e": {k: round(1e3 * v / args.steps, 3) for k, v in
+                                            zip(("batch_wait", "step_issue", "retire", "staging_issue"), e2e_phases)},
             "e2e_window": window,
             "spmm_per_callsite": spmm_detail,
             "sampler": sampler_cost,
