@@ -110,9 +110,13 @@ def parse():
                          "per batch after a host negotiation; every N > 1 run also times the other form")
     ap.add_argument("--stage-ahead", type=int, default=int(os.environ.get("GNN_STAGE_AHEAD", "1")),
                     help="batches whose X0 staging / device side are issued ahead of the current step")
-    ap.add_argument("--stage-gate", type=int, default=int(os.environ.get("GNN_STAGE_GATE", "1")),
+    ap.add_argument("--stage-gate", type=int,
+                    default=int(os.environ["GNN_STAGE_GATE"]) if "GNN_STAGE_GATE" in os.environ else None,
                     help="the next batches' X0 gathers and layer extractions wait for this layer's forward "
-                         "aggregation of the current step (an event the executor records; -1: no gate)")
+                         "aggregation of the current step (an event the executor records; -1: no gate). "
+                         "Default: 1 for graphs under 1 M nodes (Reddit: +2.4 %% end to end), none above "
+                         "(the products-shaped staging needs the whole step: 475.5 vs 441.1 without / with, "
+                         "profiles/round5/configs/)")
     ap.add_argument("--numa", default="off", choices=["gpu", "off"],
                     help="confine the process (training + producer threads) to the CPUs of the GPU's NUMA node "
                          "(A/B on one box, 3 runs each: 572 vs 584 mini-batches/s unpinned, so off by default)")
@@ -727,6 +731,8 @@ def _main(args, held):
     dropout = float(os.environ.get("GNN_BENCH_DROPOUT", "0.1"))
     model = build_model(args.model, store.F, args.nhid, [1, 1, 1], num_classes, dropout, fused=not args.unfused).to(dev)
     trainer = Trainer(model, args.lr, dev)
+    if args.stage_gate is None:
+        args.stage_gate = 1 if N < 1_000_000 else -1
     if args.stage_gate >= 0:
         gate = torch.cuda.Event()
         trainer.stage_gate = (gate, args.stage_gate)
