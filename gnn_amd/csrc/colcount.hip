@@ -19,8 +19,10 @@
 
 #include <climits>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <vector>
 
 #include "common.h"
 #include "gnn_extract.h"
@@ -160,7 +162,25 @@ int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr
   c->NB = ceil_div(num_nodes, CC_BLOCK);
   c->indptr = indptr;
   c->indices = indices;
-  GNN_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreateWithFlags");
+  // The producers' counting runs beside the training step. GNN_CC_CUS = n > 0 confines it to a
+  // stream on n of the device's CUs (spread evenly): the products-shaped GPU step then runs at
+  // 957-975 mini-batches/s instead of 450, but the producers slow down and the end-to-end rate,
+  // bound by them, drops 453 -> 404-430 (profiles/round5/configs/, r5ah) — so by default (0) the
+  // stream may use every CU.
+  int cus = 0;
+  if (const char* e = getenv("GNN_CC_CUS")) cus = atoi(e);
+  int ncu = 0;
+  GNN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
+  if (cus > 0 && cus < ncu) {
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    const int stride = ncu / cus;
+    for (int i = 0, k = 0; i < ncu && k < cus; i += stride, ++k) mask[(size_t)i / 32] |= 1u << (i % 32);
+    if (hipExtStreamCreateWithCUMask(&c->st, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      c->st = nullptr;
+    }
+  }
+  if (!c->st) GNN_HIP(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreateWithFlags");
   GNN_HIP(hipMalloc(&c->cnt, (size_t)c->N * 4), "hipMalloc");
   GNN_HIP(hipMalloc(&c->bits, (size_t)c->W * 8), "hipMalloc");
   GNN_HIP(hipMalloc(&c->blk, (size_t)c->NB * 4), "hipMalloc");
