@@ -162,16 +162,18 @@ int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr
   c->NB = ceil_div(num_nodes, CC_BLOCK);
   c->indptr = indptr;
   c->indices = indices;
-  // The producers' counting runs beside the training step. GNN_CC_CUS = n > 0 confines it to a
-  // stream on n of the device's CUs (spread evenly): the products-shaped GPU step then runs at
-  // 957-975 mini-batches/s instead of 450, but the producers slow down and the end-to-end rate,
-  // bound by them, drops 453 -> 404-430 (profiles/round5/configs/, r5ah) — so by default (0) the
-  // stream may use every CU.
+  // The producers' counting runs beside the training step. GNN_CC_CUS = n > 0 puts it on a
+  // CU-masked stream over n of the device's CUs (spread evenly; n = all CUs: a mask of every CU),
+  // which gets a hardware queue of its own: the products-shaped GPU step then runs at 957-977
+  // mini-batches/s instead of 450-480 when the two overlap — but in the end-to-end run the counts
+  // (~1.2 ms of kernels and copies per batch) then take more of the GPU from the step and the rate
+  // drops 453-470 -> 404-436 (profiles/round5/configs/, r5ah, r5an) — so by default (0) the streams
+  // are plain ones.
   int cus = 0;
   if (const char* e = getenv("GNN_CC_CUS")) cus = atoi(e);
   int ncu = 0;
   GNN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
-  if (cus > 0 && cus < ncu) {
+  if (cus > 0 && cus <= ncu) {
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     const int stride = ncu / cus;
     for (int i = 0, k = 0; i < ncu && k < cus; i += stride, ++k) mask[(size_t)i / 32] |= 1u << (i % 32);
