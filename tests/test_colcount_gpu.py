@@ -36,6 +36,7 @@ def _graph(name):
         D.data[:] = 1
         D.sort_indices()
         _G["directed"] = graphs.lap_matrix(D, "gcn")
+        _G["wide"] = graphs.lap_matrix(graphs.chung_lu(150_003, 600_000, 1.3, rng), "graphsage")  # 19 buckets
     return _G[name]
 
 
@@ -57,15 +58,24 @@ def _add(cc, rows, N):
     return live, c
 
 
-@pytest.mark.parametrize("gname", ["symmetric", "directed"])
-def test_colcount_api_matches_numpy(dev, gname):
+# the histogram's forms (colcount.hip): partitioned (default), one atomic per entry, and the
+# partitioned form whose offsets buffer is too small for the first calls (the atomic kernel runs,
+# then the buffer grows)
+_FORMS = {"part": {}, "atomic": {"GNN_CC_HIST": "atomic"}, "part-grow": {"GNN_CC_KEYS": "100"}}
+
+
+@pytest.mark.parametrize("form", list(_FORMS))
+@pytest.mark.parametrize("gname", ["symmetric", "directed", "wide"])
+def test_colcount_api_matches_numpy(dev, gname, form, monkeypatch):
+    for k, v in _FORMS[form].items():
+        monkeypatch.setenv(k, v)
     lap = _graph(gname)
     N = lap.shape[0]
     cc = sampler.ColumnCounter(lap, dev)
     try:
         rng = np.random.default_rng(1)
         acc = np.zeros(N, np.int64)
-        for step in range(3):  # counts carry over between calls
+        for step in range(4):  # counts carry over between calls
             rows = rng.integers(0, N, 500 * (step + 1))  # repeats count again
             acc += np.bincount(lap[rows].indices, minlength=N)
             live, counts = _add(cc, rows, N)
