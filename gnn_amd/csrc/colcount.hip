@@ -23,11 +23,11 @@
 // buckets per workgroup, one LDS add per run of same-bucket lanes; a chunked scan gives every
 // (bucket, workgroup) its slot range; cc_part_scatter: the 13-bit offsets written there), then one
 // workgroup per bucket adds its entries in LDS and writes its 8,192 columns' sums into cnt
-// (cc_bucket_add) — no global atomics. Its kernels take longer in isolation (≈155 µs per call
-// against 90: the partition reads every row twice), but the products-shaped end-to-end rate is 3-5 % higher
-// with it (A/B pairs on four boxes, profiles/round5/colcount_part/). The offsets buffer grows to the largest call seen: a call
-// with more entries than it holds runs the atomic kernel instead (cc_hist_guard, which does nothing
-// otherwise). GNN_CC_HIST=atomic selects the atomic form.
+// (cc_bucket_add) — no global atomics. Its kernels take longer in isolation (≈135 µs per call
+// against 90: the partition reads every row twice), but the products-shaped end-to-end rate is 4 %
+// higher with it (A/B pairs on five boxes, profiles/round5/colcount_part/). The offsets buffer
+// grows to the largest call seen: a call with more entries than it holds runs the atomic kernel
+// instead (cc_hist_guard, which does nothing otherwise). GNN_CC_HIST=atomic selects the atomic form.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,6 +73,7 @@ constexpr int CB_SHIFT = 13;                // columns per bucket: 2^13 (32 KB o
 constexpr int CB_COLS = 1 << CB_SHIFT;
 constexpr int CB_MAX = 8192;                 // buckets (32 KB of LDS in the partition kernels)
 constexpr int CP_WAVES = 4;                  // waves per partition workgroup, a wave per row
+constexpr int CP_U = 4;                      // 64-entry pieces of a row loaded at once
 
 // A row's columns are ascending, so the lanes of one 64-entry piece that fall in one bucket are
 // consecutive: each run's first lane adds the run's length (one LDS atomic per run, not per entry
@@ -111,11 +112,22 @@ __global__ __launch_bounds__(256) void cc_part_count_kernel(const int32_t* __res
   for (int r = blockIdx.x * CP_WAVES + w; r < n; r += gridDim.x * CP_WAVES) {
     const int64_t v = rows[r];
     const int64_t b = indptr[v], e = indptr[v + 1];
-    for (int64_t k0 = b; k0 < e; k0 += 64) {
-      const int nvalid = (int)(e - k0 < 64 ? e - k0 : 64);
-      const bool valid = lane < nvalid;
-      const Run ru = bucket_run(valid ? indices[k0 + lane] : 0, valid, lane, nvalid);
-      if (ru.is_head) atomicAdd(&h[ru.bk], ru.len);
+    for (int64_t k0 = b; k0 < e; k0 += 64 * CP_U) {  // CP_U pieces' loads in flight at once
+      int cu[CP_U];
+#pragma unroll
+      for (int u = 0; u < CP_U; ++u) {
+        const int64_t k = k0 + u * 64 + lane;
+        cu[u] = k < e ? indices[k] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < CP_U; ++u) {
+        const int64_t ku = k0 + u * 64;
+        if (ku >= e) break;
+        const int nvalid = (int)(e - ku < 64 ? e - ku : 64);
+        const bool valid = lane < nvalid;
+        const Run ru = bucket_run(cu[u], valid, lane, nvalid);
+        if (ru.is_head) atomicAdd(&h[ru.bk], ru.len);
+      }
     }
   }
   __syncthreads();
@@ -138,15 +150,26 @@ __global__ __launch_bounds__(256) void cc_part_scatter_kernel(const int32_t* __r
   for (int r = blockIdx.x * CP_WAVES + w; r < n; r += gridDim.x * CP_WAVES) {
     const int64_t v = rows[r];
     const int64_t b = indptr[v], e = indptr[v + 1];
-    for (int64_t k0 = b; k0 < e; k0 += 64) {
-      const int nvalid = (int)(e - k0 < 64 ? e - k0 : 64);
-      const bool valid = lane < nvalid;
-      const int c = valid ? indices[k0 + lane] : 0;
-      const Run ru = bucket_run(c, valid, lane, nvalid);
-      int base = 0;
-      if (ru.is_head) base = atomicAdd(&h[ru.bk], ru.len);
-      base = __shfl(base, valid ? ru.head : 0);
-      if (valid) keys[base + (lane - ru.head)] = (uint16_t)(c & (CB_COLS - 1));
+    for (int64_t k0 = b; k0 < e; k0 += 64 * CP_U) {
+      int cu[CP_U];
+#pragma unroll
+      for (int u = 0; u < CP_U; ++u) {
+        const int64_t k = k0 + u * 64 + lane;
+        cu[u] = k < e ? indices[k] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < CP_U; ++u) {
+        const int64_t ku = k0 + u * 64;
+        if (ku >= e) break;
+        const int nvalid = (int)(e - ku < 64 ? e - ku : 64);
+        const bool valid = lane < nvalid;
+        const int c = cu[u];
+        const Run ru = bucket_run(c, valid, lane, nvalid);
+        int base = 0;
+        if (ru.is_head) base = atomicAdd(&h[ru.bk], ru.len);
+        base = __shfl(base, valid ? ru.head : 0);
+        if (valid) keys[base + (lane - ru.head)] = (uint16_t)(c & (CB_COLS - 1));
+      }
     }
   }
 }
