@@ -23,9 +23,9 @@
 // buckets per workgroup, one LDS add per run of same-bucket lanes; a chunked scan gives every
 // (bucket, workgroup) its slot range; cc_part_scatter: the 13-bit offsets written there), then one
 // workgroup per bucket adds its entries in LDS and writes its 8,192 columns' sums into cnt
-// (cc_bucket_add) — no global atomics. Its kernels take longer in isolation (≈135 µs per call
+// (cc_bucket_add) — no global atomics. Its kernels take longer in isolation (≈130 µs per call
 // against 90: the partition reads every row twice), but the products-shaped end-to-end rate is 4 %
-// higher with it (A/B pairs on five boxes, profiles/round5/colcount_part/). The offsets buffer
+// higher with it (A/B pairs on six boxes, profiles/round5/colcount_part/). The offsets buffer
 // grows to the largest call seen: a call with more entries than it holds runs the atomic kernel
 // instead (cc_hist_guard, which does nothing otherwise). GNN_CC_HIST=atomic selects the atomic form.
 #include <hip/hip_runtime.h>
@@ -73,7 +73,7 @@ constexpr int CB_SHIFT = 13;                // columns per bucket: 2^13 (32 KB o
 constexpr int CB_COLS = 1 << CB_SHIFT;
 constexpr int CB_MAX = 8192;                 // buckets (32 KB of LDS in the partition kernels)
 constexpr int CP_WAVES = 4;                  // waves per partition workgroup, a wave per row
-constexpr int CP_U = 4;                      // 64-entry pieces of a row loaded at once
+constexpr int CP_U = 16;                     // 64-entry pieces of a row loaded at once
 
 // A row's columns are ascending, so the lanes of one 64-entry piece that fall in one bucket are
 // consecutive: each run's first lane adds the run's length (one LDS atomic per run, not per entry
