@@ -75,7 +75,10 @@ int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, const 
  *   context's counts, then return the non-zero columns: *bits = bitmap (host, ceil(N/64) words,
  *   bit c%64 of word c/64), *counts = their counts in ascending column order (host, *nlive
  *   entries). Both stay valid until the next call on the context.
- * reset: zero the counts (stream-ordered before the next add). */
+ * reset: zero the counts (stream-ordered before the next add).
+ * The counts are summed without global atomics (a bucket partition + LDS histograms) unless
+ * GNN_CC_HIST=atomic is set when the context is created; same counts either way. GNN_CC_CUS=n:
+ * the context's stream on n of the device's CUs (own hardware queue; default: a plain stream). */
 int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx);
 int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, const uint64_t** bits,
                      const int32_t** counts);
