@@ -342,6 +342,63 @@ def cpu_baseline(args, hb, feats, num_classes):
             "spmm_call_ms": calls}
 
 
+def dropin_timing(hb, feats, dev, H, reps=20):
+    """The drop-in boundary timed per call: the reference's own SparseDenseMM
+    pattern (custom_sparse_ops.py:16-37) through the `spmm` extension module — forward
+    spmm_load_balance(A, X) on a create_coo_tensor operand (spmm.cpp:23-27, 44-50), backward
+    spmm_load_balance(A.transpose(0,1).coalesce(), G) with ATen's transpose + coalesce — beside the
+    native call on the same operands (gnn_amd.custom_sparse_ops.spmm_csr on the CSR the builder
+    made, and on its GPU-built canonical transpose). Config-2 layer-0 forward and layer-1 backward
+    shapes; dense operands contiguous as the reference requires. Wall time per call over `reps`
+    calls ended by one synchronize (the drop-in backward's coalesce synchronises by itself: ATen
+    needs the unique count on the host), after one untimed call."""
+    from gnn_amd import custom_sparse_ops as cso
+    from gnn_amd import torch_ops
+
+    ext = torch_ops.load()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    def per_call(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return round(1e6 * (time.perf_counter() - t0) / reps, 1)
+
+    out = {}
+    for li, site in ((0, "fwd_L0"), (1, "bwd_L1")):
+        L = hb.layers[li]
+        M, K = L.shape
+        ins = (t(L.fullrowptr), t(L.rowptr), t(L.colidx), t(L.normfact))
+        A = ext.create_coo_tensor(*ins, M, K)
+        op, _ = cso.build_operand(*ins, M, K, with_coo=False)
+        if li == 0:
+            X = feats[torch.from_numpy(np.asarray(hb.input_nodes, np.int64))].contiguous().to(dev)
+            d_us = per_call(lambda: ext.spmm_load_balance(A, X))
+            n_us = per_call(lambda: cso.spmm_csr(op, X))
+            foreign = torch.sparse_coo_tensor(A._indices(), A._values(), A.shape, is_coalesced=True)
+            extra = {"dropin_foreign_coo_us": per_call(lambda: ext.spmm_load_balance(foreign, X)),
+                     "what": "spmm_load_balance(A, X) with A from spmm.create_coo_tensor (the CSR the builder made "
+                             "is kept on the tensor: no COO->CSR in the call); dropin_foreign_coo_us: the same "
+                             "operand as a plain torch COO tensor, converted COO->CSR on the GPU every call"}
+        else:
+            G = torch.randn(M, H, device=dev)
+            opt = op.transpose()  # built on the GPU once, kept on the operand
+            d_us = per_call(lambda: ext.spmm_load_balance(A.transpose(0, 1).coalesce(), G))
+            n_us = per_call(lambda: cso.spmm_csr(opt, G))
+            c_us = per_call(lambda: A.transpose(0, 1).coalesce())
+            extra = {"aten_transpose_coalesce_us": c_us,
+                     "what": "spmm_load_balance(A.transpose(0,1).coalesce(), G): ATen's transpose + coalesce "
+                             "(a sort, and a host sync for its unique count) every call, COO->CSR of the new "
+                             "tensor, the aggregation; native: the canonical transpose built once on the GPU"}
+        out[site] = {"dropin_us": d_us, "native_us": n_us, "overhead": round(d_us / n_us - 1.0, 4) if n_us else None,
+                     "M": int(M), "K": int(K), "nnz": int(L.colidx.size), "F": int(X.shape[1] if li == 0 else H),
+                     **extra}
+    return out
+
+
 def gpu_numa_cpus(dev) -> list:
     """The host CPUs of the GPU's NUMA node (sysfs; [] if unknown): the producer threads' blobs
     and the training thread's launches then stay on the socket the GPU hangs off."""
@@ -376,6 +433,46 @@ def cpu_budget() -> int:
     except (OSError, ValueError):
         pass
     return n
+
+
+def host_counters() -> dict:
+    """CPU-time counters of this process and of its cgroup (cgroup v2 cpu.stat: usage and the
+    CFS quota's throttling), read around a timed window."""
+    c = {"wall": time.perf_counter(), "proc_cpu": time.process_time(), "thread_cpu": time.thread_time()}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, _, v = line.partition(" ")
+                if k in ("usage_usec", "nr_periods", "nr_throttled", "throttled_usec"):
+                    c["cg_" + k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return c
+
+
+def host_delta(a: dict, b: dict) -> dict:
+    return {k: b[k] - a[k] for k in a if k in b}
+
+
+def host_report(d: dict, steps: int, workers: int) -> dict:
+    """Where the host's CPU went over a timed window, per step: the training thread, the rest of
+    the process (sampler / producer threads, HIP runtime threads), the whole cgroup, and whether the
+    cgroup's CPU quota throttled it (nr_throttled > 0: every thread stalled for the rest of a period)."""
+    if not d:
+        return None
+    ms = lambda s: round(1e3 * s / max(steps, 1), 3)
+    out = {"trainer_thread_cpu_ms_per_step": ms(d["thread_cpu"]),
+           "other_threads_cpu_ms_per_step": ms(d["proc_cpu"] - d["thread_cpu"]),
+           "process_cpus_busy": round((d["proc_cpu"]) / d["wall"], 2) if d["wall"] > 0 else None,
+           "cpu_budget": cpu_budget(), "sampler_workers": workers}
+    if "cg_usage_usec" in d:
+        out["cgroup"] = {"cpus_busy": round(d["cg_usage_usec"] * 1e-6 / d["wall"], 2) if d["wall"] > 0 else None,
+                         "periods": d.get("cg_nr_periods"), "throttled_periods": d.get("cg_nr_throttled"),
+                         "throttled_ms": round(d.get("cg_throttled_usec", 0) * 1e-3, 3)}
+    out["what"] = ("CPU time over the timed window: the training thread (HIP's blocking waits spin, so it "
+                   "reads near the wall), the process's other threads (the sampler producers and HIP's own "
+                   "threads), and the cgroup's usage and CFS-quota throttling (cpu.stat)")
+    return out
 
 
 def default_workers(world: int) -> int:
@@ -750,13 +847,20 @@ def _main(args, held):
     step_events = [] if os.environ.get("GNN_BENCH_STEP_EVENTS") == "1" else None
 
     def pipeline(next_item, steps, carry=None):
-        if compute_stream is None:
-            return _pipeline(next_item, steps, carry)
-        compute_stream.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(compute_stream):
-            loss = _pipeline(next_item, steps, carry)
-        torch.cuda.current_stream(dev).wait_stream(compute_stream)
-        return loss
+        try:
+            if compute_stream is None:
+                return _pipeline(next_item, steps, carry)
+            compute_stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(compute_stream):
+                loss = _pipeline(next_item, steps, carry)
+            torch.cuda.current_stream(dev).wait_stream(compute_stream)
+            return loss
+        finally:
+            # N > 1: the last step of a pass may have prefetched the next batch's layer 0; the pass
+            # that follows may use other batches (or none), so its workspace is not held across passes
+            ex = getattr(trainer, "executor", None)
+            if ex is not None:
+                ex.drop_prefetch()
 
     def next_batch(ahead):
         """The batch after the current one, for the trainer's layer-0 prefetch during the gradient
@@ -811,22 +915,25 @@ def _main(args, held):
             # the next batch's staging after this step's launches (its own stream: it still
             # overlaps this step, behind --stage-gate's event when set), so a timed pass's first
             # kernels start without waiting for it
-            if persistent:
-                ahead.append(stager.issue(*next_item()))
-            elif issued < steps:
-                ahead.append(stager.issue(*next_item()))
+            t4_ = t3_
+            if persistent or issued < steps:
+                item = next_item()  # the producer's next batch (blocks while it is still being sampled)
+                t4_ = time.perf_counter()
+                ahead.append(stager.issue(*item))
                 issued += 1
-            t4_ = time.perf_counter()
+            t5_ = time.perf_counter()
             ph[0] += t1_ - t0_
             ph[1] += t2_ - t1_
             ph[2] += t3_ - t2_
             ph[3] += t4_ - t3_
+            ph[4] += t5_ - t4_
         return loss
 
     lead_steps = int(os.environ.get("GNN_BENCH_LEAD", "3"))
-    # host wall time per pipeline phase (staged-batch wait, step issue, retire, next staging issue),
-    # accumulated by _pipeline and reset by timed(): where the issuing thread's time goes
-    host_phases = [0.0, 0.0, 0.0, 0.0]
+    # host wall time per pipeline phase (staged-batch wait, step issue, retire, the producer's next
+    # batch, next staging issue), accumulated by _pipeline and reset by timed(): where the issuing
+    # thread's time goes
+    host_phases = [0.0, 0.0, 0.0, 0.0, 0.0]
 
     def timed(fn_, lead=None):
         """barrier + sync on both sides, max over ranks; returns (seconds, host issue seconds).
@@ -847,7 +954,8 @@ def _main(args, held):
                 torch.distributed.barrier()
             torch.cuda.synchronize()
             retire.wait_s = 0.0
-            host_phases[:] = [0.0, 0.0, 0.0, 0.0]
+            host_phases[:] = [0.0, 0.0, 0.0, 0.0, 0.0]
+            hc0 = host_counters()
             ts = time.perf_counter()
             cpu0 = time.thread_time()
             out = fn_()
@@ -855,6 +963,7 @@ def _main(args, held):
             # the issuing thread's CPU time (HIP's blocking waits may spin: an upper bound)
             timed.cpu_s = time.thread_time() - cpu0
             timed.phases = list(host_phases)
+            timed.host = host_delta(hc0, host_counters())
             torch.cuda.synchronize()
             if world > 1:
                 torch.distributed.barrier()
@@ -914,7 +1023,7 @@ def _main(args, held):
         return out
 
     e2e_s, e2e_issue, loss = timed(e2e_window, lead=lambda: pipeline(nxt_live, min(lead_steps, warm), live_ahead))
-    e2e_cpu, e2e_phases = timed.cpu_s, timed.phases
+    e2e_cpu, e2e_phases, e2e_host = timed.cpu_s, timed.phases, timed.host
     if step_events is not None:
         evs = step_events[-args.steps:] + [w1]
         log("e2e window step spans (ms): " + " ".join(f"{a.elapsed_time(b):.3f}" for a, b in zip(evs, evs[1:])))
@@ -1146,9 +1255,15 @@ def _main(args, held):
 
     cpu = None
     sampler_cost = None
+    dropin = None
     if rank == 0 and world == 1:
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args, probe_batch, feats, num_classes)
+        if args.sampler == "ladies" and args.graph == "reddit" and not args.no_roofline:
+            try:
+                dropin = dropin_timing(probe_batch, feats, dev, 2 * args.nhid if args.model == "graphsage" else args.nhid)
+            except Exception as e:  # a failed side measurement must not sink the benchmark
+                log(f"drop-in timing skipped: {e!r}")
         chunks = sampler.rank_batches(train, args.batch_size, 0, 1, 99)[:4]
         t = time.perf_counter()
         for i, c in enumerate(chunks[:3]):
@@ -1204,9 +1319,12 @@ def _main(args, held):
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "host_cpu_ms_per_step_e2e": round(1e3 * e2e_cpu / args.steps, 3),
             "host_phases_ms_per_step_e2e": {k: round(1e3 * v / args.steps, 3) for k, v in
-                                            zip(("batch_wait", "step_issue", "retire", "staging_issue"), e2e_phases)},
+                                            zip(("batch_wait", "step_issue", "retire", "producer_wait",
+                                                 "staging_issue"), e2e_phases)},
+            "host_cpu_e2e": host_report(e2e_host, args.steps, workers),
             "e2e_window": window,
             "spmm_per_callsite": spmm_detail,
+            "dropin": dropin,
             "sampler": sampler_cost,
             "feature_staging": staging_info,
             "final_loss": round(final_loss, 5),

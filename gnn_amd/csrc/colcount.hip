@@ -28,6 +28,9 @@
 // higher with it (A/B pairs on six boxes, profiles/round5/colcount_part/). The offsets buffer
 // grows to the largest call seen: a call with more entries than it holds runs the atomic kernel
 // instead (cc_hist_guard, which does nothing otherwise). GNN_CC_HIST=atomic selects the atomic form.
+// The (bucket, workgroup) offsets are int32, so the call's entry total is also summed in int64
+// (cc_part_count) and every partition kernel checks THAT against the capacity (itself at most
+// INT32_MAX): a call of 2^31 or more entries runs the atomic form instead of wrapping an offset.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -104,14 +107,18 @@ __device__ __forceinline__ Run bucket_run(int c, bool valid, int lane, int nvali
 __global__ __launch_bounds__(256) void cc_part_count_kernel(const int32_t* __restrict__ rows, int n,
                                                              const int64_t* __restrict__ indptr,
                                                              const int32_t* __restrict__ indices, int B,
-                                                             int32_t* __restrict__ part) {
+                                                             int32_t* __restrict__ part,
+                                                             unsigned long long* __restrict__ total) {
   extern __shared__ int h[];
+  __shared__ unsigned long long wtot[CP_WAVES];
   for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long mine = 0;  // this wave's entries (the call's int64 total, below)
   for (int r = blockIdx.x * CP_WAVES + w; r < n; r += gridDim.x * CP_WAVES) {
     const int64_t v = rows[r];
     const int64_t b = indptr[v], e = indptr[v + 1];
+    mine += (unsigned long long)(e - b);
     for (int64_t k0 = b; k0 < e; k0 += 64 * CP_U) {  // CP_U pieces' loads in flight at once
       int cu[CP_U];
 #pragma unroll
@@ -130,8 +137,14 @@ __global__ __launch_bounds__(256) void cc_part_count_kernel(const int32_t* __res
       }
     }
   }
+  if (lane == 0) wtot[w] = mine;
   __syncthreads();
   for (int i = threadIdx.x; i < B; i += blockDim.x) part[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int j = 0; j < CP_WAVES; ++j) t += wtot[j];
+    atomicAdd(total, t);
+  }
 }
 
 // keys[slot] = column & (2^13 - 1), each entry at a slot of its (bucket, workgroup) range (the
@@ -141,9 +154,10 @@ __global__ __launch_bounds__(256) void cc_part_scatter_kernel(const int32_t* __r
                                                                const int64_t* __restrict__ indptr,
                                                                const int32_t* __restrict__ indices, int B,
                                                                const int32_t* __restrict__ off, int64_t cap,
+                                                               const unsigned long long* __restrict__ total,
                                                                uint16_t* __restrict__ keys) {
   extern __shared__ int h[];
-  if ((int64_t)off[(int64_t)B * gridDim.x] > cap) return;
+  if (*total > (unsigned long long)cap) return;
   for (int i = threadIdx.x; i < B; i += blockDim.x) h[i] = off[(int64_t)i * gridDim.x + blockIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -230,10 +244,10 @@ __global__ __launch_bounds__(256) void cc_chunk_add_kernel(int32_t* __restrict__
 // read-modify-write per non-zero column; the workgroup owns its columns)
 __global__ __launch_bounds__(256) void cc_bucket_add_kernel(const uint16_t* __restrict__ keys,
                                                             const int32_t* __restrict__ off, int G, int B,
-                                                            int64_t cap, int64_t N, int32_t* __restrict__ cnt) {
+                                                            int64_t cap, const unsigned long long* __restrict__ total,
+                                                            int64_t N, int32_t* __restrict__ cnt) {
   __shared__ int h[CB_COLS];
-  const int64_t total = off[(int64_t)B * G];
-  if (total > cap) return;
+  if (*total > (unsigned long long)cap) return;
   for (int i = threadIdx.x; i < CB_COLS; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const int64_t beg = off[(int64_t)blockIdx.x * G];
@@ -250,9 +264,9 @@ __global__ __launch_bounds__(256) void cc_bucket_add_kernel(const uint16_t* __re
 __global__ __launch_bounds__(256) void cc_hist_guard_kernel(const int32_t* __restrict__ rows, int n,
                                                             const int64_t* __restrict__ indptr,
                                                             const int32_t* __restrict__ indices,
-                                                            const int32_t* __restrict__ total, int64_t cap,
-                                                            int32_t* __restrict__ cnt) {
-  if ((int64_t)*total <= cap) return;
+                                                            const unsigned long long* __restrict__ total,
+                                                            int64_t cap, int32_t* __restrict__ cnt) {
+  if (*total <= (unsigned long long)cap) return;
   const int lane = threadIdx.x & 63;
   const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nwaves = (int)((gridDim.x * blockDim.x) >> 6);
@@ -327,7 +341,9 @@ struct ColCount {
   int64_t rows_cap = 0;
   int32_t* rows_h = nullptr;   // pinned [rows_cap]
   uint64_t* bits_h = nullptr;  // pinned [W]
-  int32_t* total_h = nullptr;  // pinned [2]: live columns, the call's entries (partitioned form)
+  int32_t* total_h = nullptr;  // pinned [1]: live columns
+  unsigned long long* ent = nullptr;    // device [1]: the call's entries, int64 (partitioned form)
+  unsigned long long* ent_h = nullptr;  // pinned [1]: its copy
   int32_t* out_h = nullptr;    // pinned [N]
   bool part = false;           // partitioned histogram (else the atomic one)
   int64_t B = 0;               // buckets of 2^13 columns
@@ -340,9 +356,9 @@ struct ColCount {
   ~ColCount() {
     if (st) (void)hipStreamSynchronize(st);
     for (void* p : {(void*)cnt, (void*)bits, (void*)blk, (void*)blk_off, (void*)out, (void*)rows_d, (void*)pcnt,
-                    (void*)poff, (void*)csum, (void*)keys})
+                    (void*)poff, (void*)csum, (void*)keys, (void*)ent})
       if (p) (void)hipFree(p);
-    for (void* p : {(void*)rows_h, (void*)bits_h, (void*)total_h, (void*)out_h})
+    for (void* p : {(void*)rows_h, (void*)bits_h, (void*)total_h, (void*)out_h, (void*)ent_h})
       if (p) (void)hipHostFree(p);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -423,7 +439,10 @@ int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr
   if (c->part) {
     int64_t cap = (int64_t)1 << 22;
     if (const char* e = getenv("GNN_CC_KEYS")) cap = atoll(e);
-    c->keys_cap = cap > 0 ? cap : 1;
+    c->keys_cap = cap > 0 ? std::min<int64_t>(cap, INT32_MAX) : 1;  // int32 offsets
+    GNN_HIP(hipMalloc(&c->ent, 8), "hipMalloc");
+    GNN_HIP(hipHostMalloc(&c->ent_h, 8, hipHostMallocDefault), "hipHostMalloc");
+    *c->ent_h = 0;
     GNN_HIP(hipMalloc(&c->pcnt, (size_t)(c->B * CP_GRID) * 4), "hipMalloc");
     GNN_HIP(hipMalloc(&c->poff, (size_t)(c->B * CP_GRID + 1) * 4), "hipMalloc");
     GNN_HIP(hipMalloc(&c->csum, (size_t)(ceil_div(c->B * CP_GRID, (int64_t)CS_CHUNK) + 1) * 8), "hipMalloc");
@@ -452,8 +471,9 @@ int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, 
       const int G = part_grid(n);
       const int B = (int)c->B;
       const size_t lds = (size_t)B * 4;
+      GNN_HIP(hipMemsetAsync(c->ent, 0, 8, c->st), "hipMemsetAsync");
       cc_part_count_kernel<<<dim3((unsigned)G), dim3(64 * CP_WAVES), lds, c->st>>>(c->rows_d, (int)n, c->indptr, c->indices, B,
-                                                                         c->pcnt);
+                                                                         c->pcnt, c->ent);
       GNN_LAUNCHED("cc_part_count_kernel");
       const int np = B * G, nch = (int)ceil_div(np, CS_CHUNK);
       int32_t* const coff = c->csum + nch + 1;
@@ -463,16 +483,15 @@ int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, 
       cc_chunk_add_kernel<<<dim3((unsigned)ceil_div(np, 256)), dim3(256), 0, c->st>>>(c->poff, np, coff, nch);
       GNN_LAUNCHED("cc_chunk_add_kernel");
       cc_part_scatter_kernel<<<dim3((unsigned)G), dim3(64 * CP_WAVES), lds, c->st>>>(c->rows_d, (int)n, c->indptr, c->indices,
-                                                                           B, c->poff, c->keys_cap, c->keys);
+                                                                           B, c->poff, c->keys_cap, c->ent, c->keys);
       GNN_LAUNCHED("cc_part_scatter_kernel");
-      cc_bucket_add_kernel<<<dim3((unsigned)B), dim3(256), 0, c->st>>>(c->keys, c->poff, G, B, c->keys_cap, c->N,
-                                                                       c->cnt);
+      cc_bucket_add_kernel<<<dim3((unsigned)B), dim3(256), 0, c->st>>>(c->keys, c->poff, G, B, c->keys_cap, c->ent,
+                                                                       c->N, c->cnt);
       GNN_LAUNCHED("cc_bucket_add_kernel");
       cc_hist_guard_kernel<<<dim3((unsigned)std::min<int64_t>(ceil_div(waves, 4), 512)), dim3(256), 0, c->st>>>(
-          c->rows_d, (int)n, c->indptr, c->indices, c->poff + (int64_t)B * G, c->keys_cap, c->cnt);
+          c->rows_d, (int)n, c->indptr, c->indices, c->ent, c->keys_cap, c->cnt);
       GNN_LAUNCHED("cc_hist_guard_kernel");
-      GNN_HIP(hipMemcpyAsync(c->total_h + 1, c->poff + (int64_t)B * G, 4, hipMemcpyDeviceToHost, c->st),
-              "hipMemcpyAsync");
+      GNN_HIP(hipMemcpyAsync(c->ent_h, c->ent, 8, hipMemcpyDeviceToHost, c->st), "hipMemcpyAsync");
     } else {
       cc_hist_kernel<<<dim3((unsigned)ceil_div(waves, 4)), dim3(256), 0, c->st>>>(c->rows_d, (int)n, c->indptr,
                                                                                   c->indices, c->cnt);
@@ -489,8 +508,11 @@ int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, 
   GNN_HIP(hipStreamSynchronize(c->st), "hipStreamSynchronize");
   const int64_t total = *c->total_h;
   GNN_REQUIRE(total >= 0 && total <= c->N, "gnn_colcount_add: bad live count %lld", (long long)total);
-  if (c->part && n > 0 && c->total_h[1] > c->keys_cap) {  // this call ran the atomic form: grow
-    const int64_t cap = (int64_t)c->total_h[1] + c->total_h[1] / 2;
+  if (c->part && n > 0 && *c->ent_h > (unsigned long long)c->keys_cap && c->keys_cap < INT32_MAX) {
+    // this call ran the atomic form: grow (the int32 offsets cap the buffer at INT32_MAX entries;
+    // calls beyond that keep the atomic form)
+    const unsigned long long want = *c->ent_h + *c->ent_h / 2;
+    const int64_t cap = (int64_t)std::min<unsigned long long>(want, (unsigned long long)INT32_MAX);
     GNN_HIP(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     GNN_HIP(hipFree(c->keys), "hipFree");
     c->keys = nullptr;

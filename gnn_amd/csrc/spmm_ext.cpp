@@ -118,6 +118,10 @@ at::Tensor spmm_load_balance(const at::Tensor& sparseMat, const at::Tensor& dens
 
 // spmm.cpp:44-50 -> cuda_spmm.cu:787-827: val = (float)((1.0/deg_full(row)) * (double)normfact[col]),
 // a coalesced sparse COO (int64 indices [2, nnz], float32 values) of shape (nrows, ncols).
+// Contract: the tensor is marked coalesced without a host read. A repeated (row, col) pair in the
+// inputs (never made by the reference's samplers) is merged by the first spmm_load_balance on it,
+// or by gnn_amd.custom_sparse_ops.finalize_coalesce(t); other torch operators see the unmerged
+// entries until then.
 py::object create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& rowptr, const at::Tensor& colidx,
                              const at::Tensor& normfact, int64_t nrows, int64_t ncols) {
   for (const at::Tensor* t : {&fullrowptr, &rowptr, &colidx, &normfact})
@@ -148,6 +152,12 @@ py::object create_coo_tensor(const at::Tensor& fullrowptr, const at::Tensor& row
   // .coalesce() does (cuda_spmm.cu:825).
   py::object t = py::cast(out);
   if (nrows > 0 && nnz > 1) t.attr("_gnn_dup") = py::cast(ws.view(at::kLong).narrow(0, 1, 1));
+  // The CSR the builder already made (rowptr, int32 columns; values shared with the COO), kept on
+  // the tensor with the identity of its indices: spmm_load_balance then skips the per-call COO->CSR
+  // of the reference's driver (cuda_spmm.cu:620-667). A coalesce of duplicates replaces the
+  // indices, and with them the key, so the CSR is rebuilt from the merged entries.
+  t.attr("_gnn_ext_csr") = py::make_tuple(py::cast(rp), py::cast(col32), py::int_((int64_t)(intptr_t)idx.data_ptr()),
+                                          py::int_(nnz));
   return t;
 }
 
@@ -165,7 +175,19 @@ at::Tensor resolve_duplicates(const py::object& sparse) {
 }
 
 at::Tensor spmm_load_balance_py(const py::object& sparseMat, const at::Tensor& denseMat) {
-  return spmm_load_balance(resolve_duplicates(sparseMat), denseMat);
+  at::Tensor sp = resolve_duplicates(sparseMat);
+  if (py::hasattr(sparseMat, "_gnn_ext_csr")) {  // create_coo_tensor's own CSR, if still current
+    py::tuple c = sparseMat.attr("_gnn_ext_csr").cast<py::tuple>();
+    if (sp.is_sparse() && sp.is_coalesced() && sp._nnz() == c[3].cast<int64_t>() &&
+        (int64_t)(intptr_t)sp._indices().data_ptr() == c[2].cast<int64_t>()) {
+      TORCH_CHECK(denseMat.is_cuda(), "denseMat must be a CUDA tensor");
+      TORCH_CHECK(denseMat.is_contiguous(), "denseMat must be contiguous");
+      c10::DeviceGuard guard(denseMat.device());
+      return spmm_csr(c[0].cast<at::Tensor>(), c[1].cast<at::Tensor>(), sp._values().contiguous(), sp.size(0),
+                      sp.size(1), denseMat);
+    }
+  }
+  return spmm_load_balance(sp, denseMat);
 }
 
 }  // namespace

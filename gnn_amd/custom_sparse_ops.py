@@ -193,6 +193,17 @@ def _resolve_duplicates(mat: torch.Tensor) -> None:
     mat._gnn_csr = None
 
 
+def finalize_coalesce(mat: torch.Tensor) -> torch.Tensor:
+    """Complete create_coo_tensor's deferred coalesce now (one synchronisation) and return the
+    tensor: afterwards its indices hold no repeated (row, col) pair, so any torch operator may
+    consume it. The aggregation entry points (spmm, spmm_load_balance, csr_of) call this
+    themselves; other consumers of a create_coo_tensor result whose inputs may repeat a column
+    within a row call it first. A no-op for every other tensor."""
+    if getattr(mat, "_gnn_dup", None) is not None:
+        _resolve_duplicates(mat)
+    return mat
+
+
 def csr_of(mat: "torch.Tensor | CsrOperand") -> CsrOperand:
     """CSR image of a sampled operand: cached one, or built on the GPU from a coalesced COO."""
     if isinstance(mat, CsrOperand):
@@ -472,7 +483,16 @@ def create_coo_tensor(fullrowptr, rowptr, colidx, normfact, nrows, ncols) -> tor
     """spmm.cpp:44-50 / cuda_spmm.cu:806-827: coalesced sparse COO of the sampled layer with
     value = (1/full_degree(row)) * normfact[col] (double math, fp32 store). The CSR image
     is cached on the returned tensor for the aggregation kernels. CPU inputs (all four)
-    take the config-1 CPU branch."""
+    take the config-1 CPU branch.
+
+    Coalescing contract (GPU inputs): the call reads nothing back to the host, so it stays
+    stream-ordered and graph-capturable. Columns come out ascending per row and the tensor is
+    marked coalesced. If the inputs repeat a column within a row (the reference's samplers never
+    do: LADIES' after nodes are unique, sampler.py:135-139), the repeats are summed, as the
+    reference's .coalesce() does (cuda_spmm.cu:825), by the first aggregation on the tensor or by
+    ``finalize_coalesce(t)``. Until then ``_nnz()`` / ``_indices()`` / ``_values()`` show the
+    unmerged entries: a caller that hands such a tensor to another torch operator calls
+    ``finalize_coalesce`` first."""
     ins = (fullrowptr, rowptr, colidx, normfact)
     if all(isinstance(t, torch.Tensor) and t.device.type == "cpu" for t in ins):
         return _create_coo_tensor_cpu(*ins, int(nrows), int(ncols))

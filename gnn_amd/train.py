@@ -162,17 +162,17 @@ class Trainer:
                                       stage_gate=self.stage_gate)
             if self.dp:
                 flat = self.optimizer.clip_to_flat()
+                # the all-reduce is issued first, on the collective's stream: fetching the next
+                # batch may wait on the host for its staging event (GNN_EXTRACT_CHECK=step), which
+                # must not hold the collective back on this rank. The next batch's layer-0
+                # aggregation (no parameter in it) then fills the compute stream meanwhile, and the
+                # optimizer step waits for the sum (Work.wait: a stream wait, not a host one)
+                work = torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group,
+                                                    async_op=True)
                 nxt = self._next_batch(prefetch)
                 if nxt is not None:
-                    # the all-reduce runs on the collective's stream; the next batch's layer-0
-                    # aggregation (no parameter in it) fills the compute stream meanwhile, and the
-                    # optimizer step waits for the sum (Work.wait: a stream wait, not a host one)
-                    work = torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group,
-                                                        async_op=True)
                     self.executor.prefetch(*nxt, stage_gate=self.stage_gate)
-                    work.wait()
-                else:
-                    torch.distributed.all_reduce(flat, op=torch.distributed.ReduceOp.SUM, group=self.group)
+                work.wait()
                 self.optimizer.step(clipped=True)
             else:
                 # N = 1 takes no prefetch: issuing it with the clip + Adam kernels moved to a side

@@ -78,7 +78,12 @@ int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, const 
  * reset: zero the counts (stream-ordered before the next add).
  * The counts are summed without global atomics (a bucket partition + LDS histograms) unless
  * GNN_CC_HIST=atomic is set when the context is created; same counts either way. GNN_CC_CUS=n:
- * the context's stream on n of the device's CUs (own hardware queue; default: a plain stream). */
+ * the context's stream on n of the device's CUs (own hardware queue; default: a plain stream).
+ * Note: hipExtStreamCreateWithCUMask makes a BLOCKING stream (the default is non-blocking), so
+ * with GNN_CC_CUS set the counter's work also orders against legacy null-stream work; the bench's
+ * producers issue none (torch and the library use explicit streams), off by default.
+ * A call's entry total is carried in int64; a call of 2^31 or more entries (beyond the int32
+ * partition offsets) runs the atomic form instead. */
 int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx);
 int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, const uint64_t** bits,
                      const int32_t** counts);

@@ -227,3 +227,53 @@ def test_layer0_prefetch_is_bit_identical(dev):
         for s in range(2):
             for i, (x, y) in enumerate(zip(g[s], g0[s])):
                 assert torch.equal(x, y), ("gradient differs", mode, s, i)
+
+
+def test_config2_executor_step_matches_cpu_reference(dev):
+    """VERDICT r5 (Missing #4): the step bench.py times — the native executor (gnn_train_step_f32)
+    on a BASELINE config-2 batch (Reddit-shaped graph, LADIES samp 8192 / batch 512, layers
+    extracted on the GPU as in the bench) — against the reference's CPU path on the same sampled
+    sub-graph (oracle.cpu_reference: torch.sparse.mm + the reference's modules, main.py:122-146),
+    eval mode (no dropout): loss rtol 1e-4, every parameter gradient within 1e-4 of the
+    reference in relative L2 norm (the bound test_configs_gpu.py uses at configs 3-5; the layer
+    GEMMs are split3, fp32-accurate but not bitwise fp32)."""
+    from oracle.cpu_reference import cpu_inputs, torch_spmm
+
+    from gnn_amd.models import loss as loss_fn
+
+    A, labels, feats, ncls, train, *_ = graphs.make_dataset(graphs.REDDIT, seed=0)
+    lap = graphs.lap_matrix(A, "graphsage")
+    N = A.shape[0]
+    args = (5, sampler.rank_batches(train, 512, 0, 1, 2)[0], np.array([8192] * 5), N, lap, labels, [1, 1, 1],
+            np.full(N, -1), np.zeros(N, np.int64), None, 1.0, [0])
+    hb_gpu = sampler.ladies_sample_host(*args, device_extract=True)  # the bench's form
+    hb_cpu = sampler.ladies_sample_host(*args)  # the same draw, every layer extracted on the host
+    assert [list(s) for s in hb_gpu.sampled_nodes] == [list(s) for s in hb_cpu.sampled_nodes]
+    F = feats.shape[1]
+    # the reference: CPU torch.sparse.mm path
+    adjs_c, x0_c, sampled_c, y_c = cpu_inputs(hb_cpu, feats)
+    torch.manual_seed(0)
+    ref = build_model("graphsage", F, 512, [1, 1, 1], ncls, 0.1, spmm_fn=torch_spmm)
+    ref.eval()
+    lo_r = loss_fn(ref(x0_c, adjs_c, sampled_c), y_c, True, "cpu")
+    lo_r.backward()
+    # ours: the executor on the GPU-extracted operands
+    torch.manual_seed(0)
+    net = build_model("graphsage", F, 512, [1, 1, 1], ncls, 0.1, fused=True).to(dev)
+    tr = Trainer(net, 0.01, dev)
+    assert tr.executor is not None
+    net.eval()
+    db = hb_gpu.to_device(dev, with_coo=False)
+    ld = staging.padded_ld(F)
+    x = torch.zeros((hb_gpu.num_input_nodes, ld), dtype=torch.float32)
+    x[:, :F] = feats[torch.from_numpy(np.asarray(hb_gpu.input_nodes, np.int64))]
+    x0 = x.to(dev)[:, :F]
+    assert tr.executor.supports(x0, db.adjs, db.sampled_nodes, db.labels)
+    lo = tr.executor.step(x0, db.adjs, db.sampled_nodes, db.labels)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(float(lo), float(lo_r.detach()), rtol=1e-4)
+    assert len(tr.params) == len(list(ref.parameters()))
+    for (pn, p), pr in zip(net.named_parameters(), ref.parameters()):
+        g, gr = p.grad.detach().cpu().double(), pr.grad.detach().double()
+        rel = float((g - gr).norm() / max(float(gr.norm()), 1e-30))
+        assert rel < 1e-4, f"{pn}: relative gradient error {rel:.2e}"

@@ -542,6 +542,27 @@ def test_create_coo_tensor_sums_duplicate_columns(dev):
             np.testing.assert_allclose(Y.cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(), rtol=RTOL, atol=ATOL)
 
 
+def test_finalize_coalesce_merges_before_other_consumers(dev):
+    """The documented contract: a create_coo_tensor result whose inputs repeat a column
+    is merged by finalize_coalesce before any aggregation, so torch.sparse.mm and _nnz() see the
+    reference's coalesced tensor; a second call and a foreign tensor are no-ops."""
+    M, K, full, rowptr, col, nf = duplicate_columns_case()
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ref = coalesced_reference(M, K, full, rowptr, col, nf)
+    A = cso.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int32)), t(nf), M, K)
+    assert cso.finalize_coalesce(A) is A
+    assert A._nnz() == ref._nnz() and torch.equal(A._indices().cpu(), ref._indices())
+    np.testing.assert_allclose(A._values().cpu().numpy(), ref._values().numpy(), rtol=1e-6)
+    cso.finalize_coalesce(A)
+    X = torch.randn(K, 24, device=dev)
+    np.testing.assert_allclose(torch.sparse.mm(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(),
+                               rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(cso.spmm(A, X).cpu().numpy(), torch.sparse.mm(ref, X.cpu()).numpy(),
+                               rtol=RTOL, atol=ATOL)
+    other = ref.to(dev)
+    assert cso.finalize_coalesce(other) is other
+
+
 def test_create_coo_tensor_graph_capture(dev):
     """create_coo_tensor issues no host read (the drop-in builder synced per call for its
     duplicate check): it captures into a HIP graph, and replays rebuild the operand bit-exactly

@@ -219,3 +219,27 @@ def test_module_create_coo_tensor_graph_capture(dev):
     ocol, oval = O.build_operand(full, rowptr, col, nf)
     assert np.array_equal(A._indices()[1].cpu().numpy(), ocol)
     assert np.array_equal(A._values().cpu().numpy(), oval)
+
+
+@pytest.mark.gpu
+def test_module_uses_the_builders_csr(dev):
+    """create_coo_tensor keeps the CSR its builder made on the tensor (no per-call
+    COO->CSR in spmm_load_balance); the result equals the per-call COO->CSR path on a plain torch
+    COO tensor with the same entries bit for bit, and a coalesce that merges duplicates drops it."""
+    mod = torch_ops.load()
+    full, rowptr, col, normfact, X, _ = _case(4)
+    M, K = len(rowptr) - 1, X.shape[0]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    A = mod.create_coo_tensor(t(full), t(rowptr), t(col.astype(np.int32)), t(normfact), M, K)
+    assert hasattr(A, "_gnn_ext_csr")
+    plain = torch.sparse_coo_tensor(A._indices(), A._values(), A.shape, is_coalesced=True)
+    Xd = t(X)
+    assert torch.equal(mod.spmm_load_balance(A, Xd), mod.spmm_load_balance(plain, Xd))
+    from oracle.fixtures import coalesced_reference, duplicate_columns_case
+
+    M2, K2, full2, rowptr2, col2, nf2 = duplicate_columns_case()
+    B = mod.create_coo_tensor(t(full2), t(rowptr2), t(col2.astype(np.int32)), t(nf2), M2, K2)
+    X2 = torch.randn(K2, 16, device=dev)
+    ref = coalesced_reference(M2, K2, full2, rowptr2, col2, nf2)
+    np.testing.assert_allclose(mod.spmm_load_balance(B, X2).cpu().numpy(), torch.sparse.mm(ref, X2.cpu()).numpy(),
+                               rtol=1e-5, atol=1e-5)
