@@ -614,6 +614,207 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// "split3w": the split3 kernel with twice the output per wave (round 6).
+//
+// The 128 x 128 split3 tile gives each wave a 64 x 64 output: per k16 stage 24 MFMAs against 12
+// ds_read_b128, 16 split floats per thread and one barrier. Here the tile is 128 x 256 (the same
+// 2 x 2 waves, each 64 x 128 = 2 x 4 blocks of 32 x 32): per stage 48 MFMAs against 18 reads, 24
+// split floats per thread and still one barrier — a quarter fewer LDS reads and split
+// instructions per MFMA and half the barriers. The price is the register file: 128 accumulators,
+// so two workgroups per CU (8 waves) instead of three, and LDS 72 KB per workgroup. The B operand
+// of a stage is two 128-row halves, each loaded, split and stored exactly as split3 does its B.
+// Every output element accumulates the same pieces in the same order as split3 (per k16 step the
+// six products h·h .. l·h, small terms first): whole tiles are bit-identical to split3's.
+// ---------------------------------------------------------------------------------------------
+constexpr int W_BN = 2 * BN;  // 256
+
+// piece-image chunk offset (bf16 units) for an image of R rows (split3's s3_chunk at R = 128)
+template <bool KMAJ, int R>
+__device__ __forceinline__ int s3w_chunk(int row, int h) {
+  if constexpr (KMAJ) return (h * R + row) * 8;
+  else return (2 * row + (h ^ ((row >> 3) & 1))) * 8;
+}
+
+// split 8 floats of (row rr, k half kh) into the three piece images (each R x 16 bf16)
+template <bool KMAJ, int R>
+__device__ __forceinline__ void s3w_store(unsigned short* __restrict__ S, int rr, int kh, const float v[8]) {
+  u4v ph, pm, pl;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = v[2 * j], x1 = v[2 * j + 1];
+    const unsigned int h0 = __float_as_uint(x0) & 0xffff0000u, h1 = __float_as_uint(x1) & 0xffff0000u;
+    const float r0 = x0 - __uint_as_float(h0), r1 = x1 - __uint_as_float(h1);
+    const unsigned int m0 = __float_as_uint(r0) & 0xffff0000u, m1 = __float_as_uint(r1) & 0xffff0000u;
+    const float l0 = r0 - __uint_as_float(m0), l1 = r1 - __uint_as_float(m1);
+    ph[j] = __builtin_amdgcn_perm(h1, h0, 0x07060302u);
+    pm[j] = __builtin_amdgcn_perm(m1, m0, 0x07060302u);
+    pl[j] = __builtin_amdgcn_perm(__float_as_uint(l1), __float_as_uint(l0), 0x07060302u);
+  }
+  const int off = s3w_chunk<KMAJ, R>(rr, kh);
+  *reinterpret_cast<u4v*>(S + off) = ph;
+  *reinterpret_cast<u4v*>(S + R * S3_BK + off) = pm;
+  *reinterpret_cast<u4v*>(S + 2 * R * S3_BK + off) = pl;
+}
+
+template <bool KMAJ, int R>
+__device__ __forceinline__ bf8v s3w_frag(const unsigned short* __restrict__ S, int piece, int row, int h) {
+  return __builtin_bit_cast(bf8v, *reinterpret_cast<const u4v*>(S + piece * R * S3_BK + s3w_chunk<KMAJ, R>(row, h)));
+}
+
+// one k16 step: the wave's 2 x 4 blocks, per B block its three pieces, the six products in
+// split3's order
+template <bool AK, bool BKM>
+__device__ __forceinline__ void s3w_mma(const unsigned short* __restrict__ Sa, const unsigned short* __restrict__ Sb,
+                                        int ra0, int rb0, int li, int lh, f16v acc[2][4]) {
+  bf8v a[2][3];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i][p] = s3w_frag<AK, BM>(Sa, p, ra0 + i * 32 + li, lh);
+  constexpr int PA[6] = {2, 1, 0, 1, 0, 0};
+  constexpr int PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bf8v bb[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) bb[p] = s3w_frag<BKM, W_BN>(Sb, p, rb0 + j * 32 + li, lh);
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][PA[q]], bb[PB[q]], acc[i][j], 0, 0, 0);
+  }
+}
+
+// two workgroups per CU: LDS 72 KB each, up to 256 registers (2 waves per SIMD)
+template <bool AK, bool BKM, int VA, int VB, bool IDX = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_s3w_kernel(
+    Batch bt, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int splits, int klen, float* __restrict__ part,
+    int64_t abytes, int64_t bbytes, int xcd_map) {
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][S3_OPER];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][2 * S3_OPER];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wid = t >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+  if (xcd_map) {  // consecutive tiles on one XCD (split3's map)
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    const int hw = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const int per = total >> 3;
+    const int lg = hw < per * 8 ? (hw & 7) * per + (hw >> 3) : hw;
+    tx = lg % gx;
+    ty = (lg / gx) % gy;
+    tz = lg / (gx * gy);
+  }
+  const int b = tz / splits;
+  const int split = tz % splits;
+  const int m0 = ty * BM;
+  const int n0 = tx * W_BN;
+  const int kbeg = split * klen;
+  const int kend = min(K, kbeg + klen);
+  const float* __restrict__ A = bt.A[b];
+  const float* __restrict__ B = bt.B[b];
+  const __amdgpu_buffer_rsrc_t rsa = s3_rsrc(A, abytes), rsb = s3_rsrc(B, bbytes);
+  const int64_t* __restrict__ ia = (IDX && !AK) ? bt.ia[b] : nullptr;
+  const int64_t* __restrict__ ib = (IDX && BKM) ? bt.ib[b] : nullptr;
+  const int voa = s3_voff<AK>(lda, m0, M, t, ia);
+  const int vob0 = s3_voff<BKM>(ldb, n0, N, t), vob1 = s3_voff<BKM>(ldb, n0 + BN, N, t);
+  const int ar = AK ? (t & 127) : (t >> 1), ah = AK ? (t >> 7) : (t & 1);     // A's (row, k half)
+  const int br = BKM ? (t & 127) : (t >> 1), bh = BKM ? (t >> 7) : (t & 1);  // B's, per 128-row half
+
+  f16v acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f16v(0.0f);
+
+  float ra[2][8], rb[2][16];
+  const int nfull = (kend - kbeg) / S3_BK;
+  auto load_b = [&](int k0, int half, int vob, float* xb, bool guard) {
+    if (guard) {
+      if (IDX && BKM && ib)
+        s3_load<BKM, VB, true, true>(rsb, B, ldb, vob, n0 + half * BN, N, k0, kend, t, xb, ib);
+      else
+        s3_load<BKM, VB, true>(rsb, B, ldb, vob, n0 + half * BN, N, k0, kend, t, xb);
+    } else {
+      if (IDX && BKM && ib)
+        s3_load<BKM, VB, false, true>(rsb, B, ldb, vob, n0 + half * BN, N, k0, kend, t, xb, ib);
+      else
+        s3_load<BKM, VB, false>(rsb, B, ldb, vob, n0 + half * BN, N, k0, kend, t, xb);
+    }
+  };
+  auto load_ab = [&](int kt, float(&xa)[8], float(&xb)[16]) {
+    const int k0 = kbeg + min(kt, nfull - 1) * S3_BK;
+    s3_load<AK, VA, false>(rsa, A, lda, voa, m0, M, k0, kend, t, xa);
+    load_b(k0, 0, vob0, xb, false);
+    load_b(k0, 1, vob1, xb + 8, false);
+  };
+  auto store_ab = [&](int stage, const float(&xa)[8], const float(&xb)[16]) {
+    s3w_store<AK, BM>(As[stage], ar, ah, xa);
+    s3w_store<BKM, W_BN>(Bs[stage], br, bh, xb);
+    s3w_store<BKM, W_BN>(Bs[stage], br + BN, bh, xb + 8);
+  };
+  const int li = lane & 31, lh = lane >> 5;
+  if (nfull > 0) {
+    load_ab(0, ra[0], rb[0]);
+    load_ab(1, ra[1], rb[1]);
+    store_ab(0, ra[0], rb[0]);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nfull; kt += 2) {
+      load_ab(kt + 2, ra[0], rb[0]);
+      s3w_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 128, li, lh, acc);
+      store_ab(1, ra[1], rb[1]);
+      __syncthreads();
+      load_ab(kt + 3, ra[1], rb[1]);
+      s3w_mma<AK, BKM>(As[1], Bs[1], wm * 64, wn * 128, li, lh, acc);
+      store_ab(0, ra[0], rb[0]);
+      __syncthreads();
+    }
+    if (nfull & 1) {
+      s3w_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 128, li, lh, acc);
+      __syncthreads();
+    }
+  }
+  if (kbeg + nfull * S3_BK < kend) {  // k tail
+    const int k0 = kbeg + nfull * S3_BK;
+    if (IDX && !AK && ia)
+      s3_load<AK, VA, true, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0], ia);
+    else
+      s3_load<AK, VA, true>(rsa, A, lda, voa, m0, M, k0, kend, t, ra[0]);
+    load_b(k0, 0, vob0, rb[0], true);
+    load_b(k0, 1, vob1, rb[0] + 8, true);
+    store_ab(0, ra[0], rb[0]);
+    __syncthreads();
+    s3w_mma<AK, BKM>(As[0], Bs[0], wm * 64, wn * 128, li, lh, acc);
+  }
+  float* __restrict__ Cb;
+  int64_t ldo;
+  if (splits > 1) {
+    Cb = part + (int64_t)tz * M * N;
+    ldo = N;
+  } else {
+    Cb = bt.C[b];
+    ldo = ldc;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 128 + j * 32 + li;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cb[(int64_t)m * ldo + n] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 
 // The tail tiles' k pieces summed in piece order into C: 16 workgroups per tile, a float4 of the
@@ -830,6 +1031,27 @@ int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch, int64_t slots) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
+// The wide split3 kernel (128 x 256 tiles, two workgroups per CU): GNN_GEMM_WIDE = 1 routes every
+// split3 product with N >= 256 to it, 0 (default) none. A pure function of the shape and the batch
+// count the split choice is made for, so a product launched alone (gemm_split3_as_batch) takes the
+// same kernel and k splits as inside its batch, and the workspace query agrees with the launch.
+constexpr int64_t SLOTS_S3W = 2 * 256;
+
+bool use_wide(int64_t N) {
+  const char* e = getenv("GNN_GEMM_WIDE");  // per call (tests and benches toggle it)
+  const int mode = e ? atoi(e) : 0;
+  return mode == 1 && N >= W_BN;
+}
+
+int pick_splits_wide(int64_t M, int64_t N, int64_t K, int nbatch) {
+  if (const char* e = getenv("GNN_GEMM_SPLITS")) return std::max(1, atoi(e));
+  const int64_t tiles = ceil_div(M, (int64_t)BM) * ceil_div(N, (int64_t)W_BN) * nbatch;
+  if (tiles * 2 > SLOTS_S3W) return 1;
+  int64_t s = SLOTS_S3W / tiles;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, K / 256));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
+}
+
 // Tail tiles (split3, unsplit k): a launch of T tiles over 256 CUs whose last partial round holds
 // only rem = T mod 256 tiles (the layer-1 forward's 544 = 2 x 256 + 32) pays for that round almost
 // like a full one (scripts/gemm_tiles_probe.py: 512 tiles 104 us, 544 126 us, 768 139 us). The
@@ -923,6 +1145,59 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
     algo = ALGO_F32;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (algo == ALGO_S3 && K > 0 && use_wide(N)) {
+    const int splits = pick_splits_wide(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch);
+    int xcdm = 1;
+    if (const char* e = getenv("GNN_GEMM_XCD")) xcdm = atoi(e) != 0;
+    const int klen = splits > 1 ? (int)(ceil_div(ceil_div(K, (int64_t)splits), (int64_t)S3_BK) * S3_BK) : (int)K;
+    if (splits > 1) {
+      const size_t need = (size_t)splits * nbatch * M * N * sizeof(float);
+      GNN_REQUIRE(workspace && workspace_bytes >= need, "gnn_gemm_f32: workspace too small (%zu < %zu)",
+                  workspace_bytes, need);
+    }
+    const dim3 grid((unsigned)ceil_div(N, (int64_t)W_BN), (unsigned)ceil_div(M, (int64_t)BM),
+                    (unsigned)(nbatch * splits));
+    float* part = (float*)workspace;
+#define GNN_GEMMW_LAUNCH(AK, BK, VA, VB)                                                                        \
+  do {                                                                                                          \
+    if (idx)                                                                                                    \
+      gemm_s3w_kernel<AK, BK, VA, VB, true><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb,   \
+                                                                        ldc, splits, klen, part, abytes, bbytes, \
+                                                                        xcdm);                                   \
+    else                                                                                                        \
+      gemm_s3w_kernel<AK, BK, VA, VB><<<grid, dim3(256), 0, st>>>(bt, (int)M, (int)N, (int)K, lda, ldb, ldc,    \
+                                                                  splits, klen, part, abytes, bbytes, xcdm);    \
+  } while (0)
+#define GNN_GEMMW_V(AK, BK)                                    \
+  do {                                                         \
+    if (va == 4 && vb == 4) GNN_GEMMW_LAUNCH(AK, BK, 4, 4);    \
+    else if (va == 4) GNN_GEMMW_LAUNCH(AK, BK, 4, 2);          \
+    else if (vb == 4) GNN_GEMMW_LAUNCH(AK, BK, 2, 4);          \
+    else GNN_GEMMW_LAUNCH(AK, BK, 2, 2);                       \
+  } while (0)
+    if (a_kmajor && b_kmajor) GNN_GEMMW_V(true, true);
+    else if (a_kmajor) GNN_GEMMW_V(true, false);
+    else if (b_kmajor) GNN_GEMMW_V(false, true);
+    else GNN_GEMMW_V(false, false);
+#undef GNN_GEMMW_V
+#undef GNN_GEMMW_LAUNCH
+    GNN_LAUNCHED("gemm_s3w_kernel");
+    if (splits > 1) {
+      const int64_t total = (int64_t)M * N * nbatch;
+      bool vec4 = ldc == N && (M * N) % 4 == 0;
+      for (int b = 0; b < nbatch; ++b) vec4 = vec4 && (uintptr_t)C[b] % 16 == 0;
+      if (vec4) {
+        const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total / 4, (int64_t)256), 2048);
+        gemm_splitk_reduce4_kernel<<<dim3(g), dim3(256), 0, st>>>(bt, part, M * N, splits, nbatch);
+        GNN_LAUNCHED("gemm_splitk_reduce4_kernel");
+      } else {
+        const unsigned g = (unsigned)std::min<int64_t>(ceil_div(total, (int64_t)256), 2048);
+        gemm_splitk_reduce_kernel<<<dim3(g), dim3(256), 0, st>>>(bt, part, (int)M, (int)N, ldc, splits, nbatch);
+        GNN_LAUNCHED("gemm_splitk_reduce_kernel");
+      }
+    }
+    return 0;
+  }
   const int splits = K == 0 ? 1 : pick_splits(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch, slots_of(algo));
   // XCD-aware tile map for split3 (2-8 % per layer pair, scripts/gemm_bench.py); GNN_GEMM_XCD=0 turns it off
   int xcdm = 1;
@@ -1012,6 +1287,10 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 
 size_t workspace_bytes_of(int algo, int64_t M, int64_t N, int64_t K, int nbatch) {
   if (M <= 0 || N <= 0 || K <= 0 || nbatch <= 0) return 0;
+  if (algo == ALGO_S3 && use_wide(N)) {
+    const int s = pick_splits_wide(M, N, K, nbatch);
+    return s > 1 ? (size_t)s * nbatch * M * N * sizeof(float) : 0;
+  }
   const int s = pick_splits(M, N, K, nbatch, slots_of(algo));
   if (s > 1) return (size_t)s * nbatch * M * N * sizeof(float);
   return algo == ALGO_S3 ? tail_bytes(tail_plan(M, N, K, nbatch)) : 0;  // whatever GNN_GEMM_TAIL says

@@ -227,3 +227,33 @@ def test_split3_tail_tiles(dev, monkeypatch):
     assert torch.equal(on[0], off[0]) and torch.equal(on[1][:7680], off[1][:7680])
     d = (on[1][7680:] - off[1][7680:]).abs().max().item()
     assert 0 < d <= 1e-4 * off[1][7680:].abs().max().item()
+
+
+@pytest.mark.parametrize("a_km,b_km", [(False, False), (False, True), (True, True), (True, False)])
+@pytest.mark.parametrize("M,N,K,nb", [(300, 256, 77, 1), (130, 513, 602, 2), (257, 700, 1024, 1), (512, 602, 5000, 2),
+                                      (1000, 512, 33, 2)])
+def test_split3_wide_fp64_bound_and_whole_tiles_bit_identical(dev, monkeypatch, a_km, b_km, M, N, K, nb):
+    """The wide split3 kernel (GNN_GEMM_WIDE=1: 128 x 256 tiles, a wave owns 64 x 128) within the fp64
+    bound on every layout, edge tiles, split-k and batches; where it runs k unsplit (every shape
+    here but the long-k one) each output sums the same pieces in the same order as split3, so it
+    must be bit-identical to split3 with its tail tiles off."""
+    monkeypatch.setenv("GNN_GEMM_WIDE", "1")
+    _check(a_km, b_km, M, N, K, nb, dev, algo="split3")
+    g = torch.Generator().manual_seed(5)
+    As = [_operand(a_km, K if a_km else M, M if a_km else K, M if a_km else K, g, dev) for _ in range(nb)]
+    Bs = [_operand(b_km, K if b_km else N, N if b_km else K, N if b_km else K, g, dev) for _ in range(nb)]
+    wide = gemm(a_km, b_km, As, Bs, M, N, K, algo="split3")
+    monkeypatch.setenv("GNN_GEMM_WIDE", "0")
+    monkeypatch.setenv("GNN_GEMM_TAIL", "0")
+    base = gemm(a_km, b_km, As, Bs, M, N, K, algo="split3")
+    torch.cuda.synchronize()
+    if K < 4000:  # neither kernel splits k here
+        for x, y in zip(wide, base):
+            assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("case", ["a_fwd", "b_wgrad"])
+def test_split3_wide_row_indexed_equals_gathered(dev, monkeypatch, case):
+    """The wide kernel's indexed operands (x[sampled] read in place) equal the gathered operand bit for bit."""
+    monkeypatch.setenv("GNN_GEMM_WIDE", "1")
+    test_split3_row_indexed_equals_gathered(dev, case, 4100, 512, 602, 6000)
