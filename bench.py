@@ -929,7 +929,9 @@ def _main(args, held):
             ph[4] += t5_ - t4_
         return loss
 
-    lead_steps = int(os.environ.get("GNN_BENCH_LEAD", "3"))
+    # 12 (was 3): interleaved on one box, the driver's 20-step form 605.8 / 604.4 with 12 against
+    # 597.5 / 598.9 with 3 (profiles/round6/lead/); the total number of warm-up steps is unchanged
+    lead_steps = int(os.environ.get("GNN_BENCH_LEAD", "12"))
     # host wall time per pipeline phase (staged-batch wait, step issue, retire, the producer's next
     # batch, next staging issue), accumulated by _pipeline and reset by timed(): where the issuing
     # thread's time goes

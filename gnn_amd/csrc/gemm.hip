@@ -1031,16 +1031,26 @@ int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch, int64_t slots) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
-// The wide split3 kernel (128 x 256 tiles, two workgroups per CU): GNN_GEMM_WIDE = 1 routes every
-// split3 product with N >= 256 to it, 0 (default) none. A pure function of the shape and the batch
-// count the split choice is made for, so a product launched alone (gemm_split3_as_batch) takes the
-// same kernel and k splits as inside its batch, and the workspace query agrees with the launch.
+// The wide split3 kernel (128 x 256 tiles, two workgroups per CU). Measured per layer pair against
+// split3 (scripts/gemm_bench.py, profiles/round6/gemm_wide/): the same rate per CU, so it wins only
+// where its tile count fills the chip's 512 slots once while split3's 128 x 128 tiles need a second,
+// partial round — the layer-0 forward (496 wide tiles against 992 on 768 slots: 118.8 vs 130.7 µs);
+// it loses where it leaves half the slots empty (layer-1 forward, 272 tiles: 146.6 vs 101.6 µs) or
+// spills into a second round (layer-1 input gradient, 544: 133.4 vs 109.1). Default (GNN_GEMM_WIDE
+// unset or -1): wide when k is not split and its tiles fill 85-100 % of the slots; 1: every product
+// with N >= 256; 0: never. A pure function of the shape and the batch count the split choice is made
+// for, so a product launched alone (gemm_split3_as_batch) takes the same kernel and k splits as inside
+// its batch, and the workspace query agrees with the launch.
 constexpr int64_t SLOTS_S3W = 2 * 256;
 
-bool use_wide(int64_t N) {
+bool use_wide(int64_t M, int64_t N, int64_t K, int nbatch) {
   const char* e = getenv("GNN_GEMM_WIDE");  // per call (tests and benches toggle it)
-  const int mode = e ? atoi(e) : 0;
-  return mode == 1 && N >= W_BN;
+  const int mode = e ? atoi(e) : -1;
+  if (mode == 0 || N < W_BN || K <= 0) return false;
+  if (mode == 1) return true;
+  if (getenv("GNN_GEMM_SPLITS")) return false;  // split experiments keep split3
+  const int64_t tw = ceil_div(M, (int64_t)BM) * ceil_div(N, (int64_t)W_BN) * nbatch;
+  return tw * 100 >= SLOTS_S3W * 85 && tw <= SLOTS_S3W;
 }
 
 int pick_splits_wide(int64_t M, int64_t N, int64_t K, int nbatch) {
@@ -1145,7 +1155,7 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
     algo = ALGO_F32;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (algo == ALGO_S3 && K > 0 && use_wide(N)) {
+  if (algo == ALGO_S3 && K > 0 && use_wide(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch)) {
     const int splits = pick_splits_wide(M, N, K, split_nbatch > 0 ? split_nbatch : nbatch);
     int xcdm = 1;
     if (const char* e = getenv("GNN_GEMM_XCD")) xcdm = atoi(e) != 0;
@@ -1287,7 +1297,7 @@ int gemm_run(int algo, int a_kmajor, int b_kmajor, int64_t M, int64_t N, int64_t
 
 size_t workspace_bytes_of(int algo, int64_t M, int64_t N, int64_t K, int nbatch) {
   if (M <= 0 || N <= 0 || K <= 0 || nbatch <= 0) return 0;
-  if (algo == ALGO_S3 && use_wide(N)) {
+  if (algo == ALGO_S3 && use_wide(M, N, K, nbatch)) {
     const int s = pick_splits_wide(M, N, K, nbatch);
     return s > 1 ? (size_t)s * nbatch * M * N * sizeof(float) : 0;
   }
