@@ -46,6 +46,7 @@ _SIGNATURES = {
     "gnn_csr_transpose_workspace_bytes": (_SZ, [_I64, _I64, _I64]),
     "gnn_csr_transpose": (_INT, [_VP, _VP, _VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP, _SZ, _VP]),
     "gnn_gather_rows_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
+    "gnn_gather_rows2_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
     "gnn_gather_rows_host_f32": (_INT, [_VP, _I64, _VP, _VP, _I64, _VP, _I64, _I64, _VP]),
     "gnn_host_register": (_INT, [_VP, _SZ]),
     "gnn_host_unregister": (_INT, [_VP]),

@@ -1152,6 +1152,47 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restric
   }
 }
 
+// X0 from two sources in one launch (round 6): rows [0, n0) from (src0, idx0) and
+// rows [n0, n0 + n1) from (src1, idx1), to dst rows pos0 / pos1 — the own feature-buffer rows and
+// the batch's host rows of a staging issue. A wave per row with every load of the row issued
+// before its stores (608-float rows: 3 float4 per lane).
+template <int VW, int NL>
+__global__ __launch_bounds__(256) void gather_rows2_kernel(const float* __restrict__ src0, int64_t ld0,
+                                                           const int64_t* __restrict__ idx0,
+                                                           const int64_t* __restrict__ pos0, int64_t n0,
+                                                           const float* __restrict__ src1, int64_t ld1,
+                                                           const int64_t* __restrict__ idx1,
+                                                           const int64_t* __restrict__ pos1, int64_t n1,
+                                                           float* __restrict__ dst, int64_t ld_dst, int F) {
+  using V = typename Vec<VW>::T;
+  const int lane = threadIdx.x & 63;
+  int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n0 + n1) return;
+  const bool second = i >= n0;  // wave-uniform
+  if (second) i -= n0;
+  const float* sr;
+  int64_t d;
+  if (!second) {
+    sr = src0 + (idx0 ? idx0[i] : i) * ld0;
+    d = pos0 ? pos0[i] : i;
+  } else {
+    sr = src1 + (idx1 ? idx1[i] : i) * ld1;
+    d = pos1 ? pos1[i] : i;
+  }
+  float* dr = dst + d * ld_dst;
+  V v[NL];
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int c = (lane + 64 * k) * VW;
+    if (c < F) v[k] = *reinterpret_cast<const V*>(sr + c);
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int c = (lane + 64 * k) * VW;
+    if (c < F) *reinterpret_cast<V*>(dr + c) = v[k];
+  }
+}
+
 // Rows read straight from pinned, device-mapped host memory (zero-copy over PCIe): a small
 // persistent grid (each wave two rows per pass, every load of both rows issued before the
 // first store) keeps a few MB of PCIe reads in flight while holding few CU slots, so the
@@ -1860,6 +1901,37 @@ int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx
       break;
   }
   GNN_LAUNCHED("gather_rows_kernel");
+  return 0;
+}
+
+int gnn_gather_rows2_f32(const float* src0, int64_t ld0, const int64_t* idx0, const int64_t* pos0, int64_t n0,
+                         const float* src1, int64_t ld1, const int64_t* idx1, const int64_t* pos1, int64_t n1,
+                         float* dst, int64_t ld_dst, int64_t F, void* stream) {
+  GNN_REQUIRE(n0 >= 0 && n1 >= 0 && F >= 0, "gnn_gather_rows2_f32: negative size");
+  GNN_REQUIRE(F < INT_MAX && n0 + n1 < (int64_t)INT_MAX * 4, "gnn_gather_rows2_f32: too large");
+  if (n0 + n1 == 0 || F == 0) return 0;
+  GNN_REQUIRE(dst && (n0 == 0 || src0) && (n1 == 0 || src1), "gnn_gather_rows2_f32: NULL src/dst");
+  GNN_REQUIRE(F <= ld_dst && (n0 == 0 || F <= ld0) && (n1 == 0 || F <= ld1),
+              "gnn_gather_rows2_f32: F exceeds a row stride");
+  hipStream_t st = (hipStream_t)stream;
+  // 16-byte loads when every row of both sources and of dst allows them
+  int vw = pick_vw(F, n0 ? ld0 : ld1, ld_dst, n0 ? src0 : src1, dst);
+  if (n0 && n1) vw = std::min(vw, pick_vw(F, ld1, ld_dst, src1, dst));
+  const dim3 grid((unsigned)ceil_div(n0 + n1, (int64_t)4));
+  const int per = (int)ceil_div(F, (int64_t)64 * vw);  // loads per lane
+#define GNN_G2(VW, NL) \
+  gather_rows2_kernel<VW, NL><<<grid, dim3(256), 0, st>>>(src0, ld0, idx0, pos0, n0, src1, ld1, idx1, pos1, n1, dst, ld_dst, (int)F)
+  if (vw == 4 && per <= 3) GNN_G2(4, 3);
+  else if (vw == 4 && per <= 8) GNN_G2(4, 8);
+  else if (vw == 2 && per <= 8) GNN_G2(2, 8);
+  else if (vw == 1 && per <= 16) GNN_G2(1, 16);
+  else {  // wide rows: the one-source kernel per source
+    const int rc = gnn_gather_rows_f32(src0, ld0, idx0, dst, ld_dst, pos0, n0, F, stream);
+    if (rc) return rc;
+    return gnn_gather_rows_f32(src1, ld1, idx1, dst, ld_dst, pos1, n1, F, stream);
+  }
+#undef GNN_G2
+  GNN_LAUNCHED("gather_rows2_kernel");
   return 0;
 }
 

@@ -546,6 +546,28 @@ def gather_rows(src: torch.Tensor, src_idx: Optional[torch.Tensor], dst: torch.T
                    "gnn_gather_rows_f32")
 
 
+def gather_rows2(src0: torch.Tensor, idx0: Optional[torch.Tensor], pos0: Optional[torch.Tensor], n0: int,
+                 src1: torch.Tensor, idx1: Optional[torch.Tensor], pos1: Optional[torch.Tensor], n1: int,
+                 dst: torch.Tensor) -> None:
+    """dst[pos0] = src0[idx0] (n0 rows) and dst[pos1] = src1[idx1] (n1 rows) in one launch
+    (gnn_gather_rows2_f32): X0's own-buffer and host rows."""
+    for t in (src0, src1, dst):
+        _require(t.is_cuda and t.dtype == torch.float32 and t.stride(1) == 1,
+                 "gather_rows2 tensors must be float32 CUDA tensors with contiguous rows")
+    for t in (idx0, pos0, idx1, pos1):
+        if t is not None:
+            _require(t.is_cuda and t.dtype == torch.int64 and t.is_contiguous(), "gather_rows2 indices must be int64 CUDA")
+    F = dst.shape[1]
+    _require(src0.shape[1] >= F and src1.shape[1] >= F, "gather_rows2: source rows narrower than destination")
+    F = min(_padded_width(src0, dst, F), _padded_width(src1, dst, F))
+    dev = dst.device
+    with _lib.on_device(dev):
+        _lib.check(_lib.lib().gnn_gather_rows2_f32(src0.data_ptr(), src0.stride(0), _ptr(idx0), _ptr(pos0), int(n0),
+                                                   src1.data_ptr(), src1.stride(0), _ptr(idx1), _ptr(pos1), int(n1),
+                                                   dst.data_ptr(), dst.stride(0), F, _stream(dev)),
+                   "gnn_gather_rows2_f32")
+
+
 def gather_rows_host(host: torch.Tensor, src_idx: torch.Tensor, dst: torch.Tensor,
                      dst_idx: Optional[torch.Tensor], n: Optional[int] = None) -> None:
     """dst[dst_idx] = host[src_idx], read by the GPU over PCIe from a host table registered

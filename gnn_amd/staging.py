@@ -217,9 +217,15 @@ class Stager:
                 # below wait for the gate the step records after its layer-0 aggregation, so they run
                 # beside the MFMA-bound GEMMs and tails instead of competing for L2 with the gather
                 st.wait_event(self.gate)
-            cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
-            if nh and (plan.host_rows is not None or (plan.blob is not None and not self.store.zero_copy)):
-                cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
+            host_rows_here = nh and (plan.host_rows is not None or (plan.blob is not None and not self.store.zero_copy))
+            if host_rows_here and _GATHER2:
+                # the own-buffer rows and the host rows in one launch (gnn_gather_rows2_f32)
+                cso.gather_rows2(self.store.gpu_buffer, own_src, own_pos, len(plan.own_pos), host_dev, None, host_pos,
+                                 nh, x0)
+            else:
+                cso.gather_rows(self.store.gpu_buffer, own_src, x0, own_pos, n=len(plan.own_pos))
+                if host_rows_here:
+                    cso.gather_rows(host_dev, None, x0, host_pos, n=nh)
             extra = ()
             if self.exchange is not None:
                 extra = self.exchange.exchange(plan, x0, self.store, meta)
@@ -233,6 +239,8 @@ class Stager:
 
 
 _EXTRACT_CHECK = os.environ.get("GNN_EXTRACT_CHECK", "step")
+# X0's own-buffer and host rows in one gather launch (GNN_GATHER2=0: two launches, the round-5 form)
+_GATHER2 = os.environ.get("GNN_GATHER2", "1") != "0"
 
 
 class StagedX0:

@@ -171,6 +171,13 @@ int gnn_gather_rows_f32(const float* src, int64_t ld_src, const int64_t* src_idx
                         float* dst, int64_t ld_dst, const int64_t* dst_idx,
                         int64_t n, int64_t F, void* stream);
 
+/* Two sources in one launch (round 6): dst[pos0[i]] = src0[idx0[i]] for i < n0, then
+ * dst[pos1[i]] = src1[idx1[i]] for i < n1 — the own feature-buffer rows and the batch's host
+ * rows of one X0 (main.py:129-134). NULL idx / pos = identity. */
+int gnn_gather_rows2_f32(const float* src0, int64_t ld0, const int64_t* idx0, const int64_t* pos0, int64_t n0,
+                         const float* src1, int64_t ld1, const int64_t* idx1, const int64_t* pos1, int64_t n1,
+                         float* dst, int64_t ld_dst, int64_t F, void* stream);
+
 /* Zero-copy variant for the non-buffered rows (replaces the pageable
  * feat_data[idx_cpu].to(device) of main.py:134): `host_src` is host memory registered with
  * gnn_host_register (pinned, device-mapped); the GPU reads the rows over PCIe, so no host

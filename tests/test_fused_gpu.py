@@ -303,3 +303,28 @@ def test_dropout_mask_past_2_32_elements(dev):
     ref = _keep_mask_ref(99, e, 0.25).reshape(4, D)
     assert np.array_equal(rows != 0, ref)
     assert np.all(rows[ref] == np.float32(1.0) / np.float32(0.75))
+
+
+@pytest.mark.parametrize("grid", [1, 7, 1024])
+@pytest.mark.parametrize("M,bias", [(15809, True), (1000, False), (3, True)])
+def test_sage_norm_fwd_row_walking_form_is_bit_identical(dev, monkeypatch, grid, M, bias):
+    """GNN_SAGE_FWD_PIPE=G (waves walk rows with the next row's loads in flight, on at most G
+    workgroups) against the one-row-per-wave kernel: outputs, means and rstds bit for bit, with
+    dropout (training) on."""
+    g = torch.Generator().manual_seed(M + grid)
+    hB = torch.randn(M, 512, generator=g).to(dev)
+    hW = torch.randn(M, 512, generator=g).to(dev)
+    scale = (torch.rand(1024, generator=g) + 0.5).to(dev)
+    offset = torch.randn(1024, generator=g).to(dev)
+    bB = torch.randn(512, generator=g).to(dev) if bias else None
+    bW = torch.randn(512, generator=g).to(dev) if bias else None
+    outs = []
+    for pipe in (None, str(grid)):
+        if pipe is None:
+            monkeypatch.delenv("GNN_SAGE_FWD_PIPE", raising=False)
+        else:
+            monkeypatch.setenv("GNN_SAGE_FWD_PIPE", pipe)
+        torch.manual_seed(9)
+        outs.append(sage_norm(hB, hW, scale, offset, p=0.1, training=True, biasB=bB, biasW=bW).detach())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])

@@ -143,3 +143,27 @@ def test_retirement_pipeline_on_priority_stream_matches(dev):
     assert got_l == ref_l
     for a, b in zip(got_p, ref_p):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("F,ld0,ld1,ldd", [(602, 608, 608, 608), (602, 602, 608, 602), (100, 100, 100, 100),
+                                           (1024, 1024, 1024, 1024), (3000, 3000, 3000, 3000)])
+@pytest.mark.parametrize("n0,n1", [(900, 1300), (0, 17), (33, 0)])
+def test_gather_rows2_matches_indexing(dev, F, ld0, ld1, ldd, n0, n1):
+    """gnn_gather_rows2_f32 (X0's own-buffer and host rows in one launch) against torch indexing,
+    bit for bit; padded and unpadded strides, one empty source, rows too wide for one pass."""
+    from gnn_amd import custom_sparse_ops as cso
+
+    g = torch.Generator().manual_seed(F + n0 + n1)
+    src0 = torch.randn(2000, ld0, generator=g).to(dev)
+    src1 = torch.randn(max(n1, 1), ld1, generator=g).to(dev)
+    perm = torch.randperm(n0 + n1, generator=g)
+    pos0, pos1 = perm[:n0].to(dev), perm[n0:].to(dev)
+    idx0 = torch.randint(0, 2000, (n0,), generator=g).to(dev)
+    dst = torch.full((n0 + n1, ldd), float("nan"), device=dev)
+    cso.gather_rows2(src0[:, :F], idx0, pos0, n0, src1[:, :F], None, pos1, n1, dst[:, :F])
+    torch.cuda.synchronize()
+    ref = torch.empty(n0 + n1, F, device=dev)
+    ref[pos0] = src0[idx0, :F]
+    if n1:
+        ref[pos1] = src1[:n1, :F]
+    assert torch.equal(dst[:, :F], ref)
