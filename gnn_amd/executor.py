@@ -227,6 +227,10 @@ class NativeStep:
         d[H_X0], d[H_LDX0], d[H_F0] = x0.data_ptr(), x0.stride(0) if x0.shape[0] > 1 else x0.shape[1], x0.shape[1]
         d[H_LABELS], d[H_LDL] = labels.data_ptr(), labels.stride(0) if labels.shape[0] > 1 else labels.shape[1]
         d[H_TRAINING] = int(tr)
+        # the Python path draws one seed per layer tail, then one for the head (fused.py): one
+        # randint call for all of them gives the same values from the CPU generator (one call
+        # instead of nl + 1: ~15 us less host issue per step)
+        sv = torch.randint(0, 2**62, (len(adjs) + 1,)).tolist() if (tr and seeds) else None
         for li, op in enumerate(adjs):
             b = HEADER + li * LAYER_SLOTS
             d[b + L_ROWPTR], d[b + L_COL], d[b + L_VAL] = op.rowptr.data_ptr(), op.col.data_ptr(), op.val.data_ptr()
@@ -239,9 +243,8 @@ class NativeStep:
                 d[b + L_SAMPLED], d[b + L_NSAMPLED] = s.data_ptr(), s.numel()
                 r = getattr(s, "_gnn_rmap", None)
                 d[b + L_RMAP] = _p(r) if li >= 1 else 0
-            # the Python path draws one seed per layer tail, then one for the head (fused.py)
-            d[b + L_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if (tr and seeds) else 0
-        d[H_HEAD_SEED] = int(torch.randint(0, 2**62, (1,)).item()) if (tr and seeds) else 0
+            d[b + L_SEED] = sv[li] if sv is not None else 0
+        d[H_HEAD_SEED] = sv[len(adjs)] if sv is not None else 0
         return d
 
     @staticmethod
