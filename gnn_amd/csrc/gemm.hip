@@ -1036,16 +1036,18 @@ int pick_splits(int64_t M, int64_t N, int64_t K, int nbatch, int64_t slots) {
 // where its tile count fills the chip's 512 slots once while split3's 128 x 128 tiles need a second,
 // partial round — the layer-0 forward (496 wide tiles against 992 on 768 slots: 118.8 vs 130.7 µs);
 // it loses where it leaves half the slots empty (layer-1 forward, 272 tiles: 146.6 vs 101.6 µs) or
-// spills into a second round (layer-1 input gradient, 544: 133.4 vs 109.1). Default (GNN_GEMM_WIDE
-// unset or -1): wide when k is not split and its tiles fill 85-100 % of the slots; 1: every product
-// with N >= 256; 0: never. A pure function of the shape and the batch count the split choice is made
+// spills into a second round (layer-1 input gradient, 544: 133.4 vs 109.1). In the training step the
+// layer-0 gain does not survive the staging kernels beside it (their 58 KB LDS tables leave room for
+// one 72 KB wide workgroup per CU: 175 µs under rocprofv3 against split3's 144; gpu_step 603.9 / 604.9
+// vs 603.0 / 602.6 interleaved), so the default is off. GNN_GEMM_WIDE = -1: wide when k is not split
+// and its tiles fill 85-100 % of the slots; 1: every product with N >= 256; 0 (default): never. A pure function of the shape and the batch count the split choice is made
 // for, so a product launched alone (gemm_split3_as_batch) takes the same kernel and k splits as inside
 // its batch, and the workspace query agrees with the launch.
 constexpr int64_t SLOTS_S3W = 2 * 256;
 
 bool use_wide(int64_t M, int64_t N, int64_t K, int nbatch) {
   const char* e = getenv("GNN_GEMM_WIDE");  // per call (tests and benches toggle it)
-  const int mode = e ? atoi(e) : -1;
+  const int mode = e ? atoi(e) : 0;
   if (mode == 0 || N < W_BN || K <= 0) return false;
   if (mode == 1) return true;
   if (getenv("GNN_GEMM_SPLITS")) return false;  // split experiments keep split3

@@ -329,90 +329,6 @@ __global__ __launch_bounds__(256) void sage_norm_fwd_kernel(const float* __restr
   }
 }
 
-// The same tail, each wave walking rows r, r + stride, ... with the next row's loads issued before
-// the current row is computed (round 6): one row per wave leaves a wave's load latency, its two
-// wave reductions and its stores in series, so the kernel ran at ~3 TB/s. Per element the same
-// operations in the same order as sage_norm_fwd_kernel: bit-identical outputs.
-template <int NV>
-__global__ __launch_bounds__(256) void sage_norm_fwd_pipe_kernel(const float* __restrict__ hB, int64_t ldb,
-                                                                 const float* __restrict__ bB, int D1,
-                                                                 const float* __restrict__ hW, int64_t ldw,
-                                                                 const float* __restrict__ bW, int D,
-                                                                 const float* __restrict__ scale,
-                                                                 const float* __restrict__ offset, int M, float p,
-                                                                 float inv_keep, uint64_t seed, int training,
-                                                                 float* __restrict__ Y, int64_t ldy,
-                                                                 float* __restrict__ mean_out,
-                                                                 float* __restrict__ rstd_out) {
-  const int lane = threadIdx.x & 63;
-  const int stride = gridDim.x * 4;
-  int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  f4 hn[NV];
-  auto load_row = [&](int rr) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (lane + 64 * k) * 4;
-      hn[k] = c < D ? load_h(hB, ldb, bB, D1, hW, ldw, bW, rr, c) : f4(0.0f);
-    }
-  };
-  if (r < M) load_row(r);
-  const DropThr dt = drop_thr(p);
-  const uint32_t key = drop_key(seed);
-  while (r < M) {
-    f4 o[NV];
-#pragma unroll
-    for (int k = 0; k < NV; ++k) o[k] = hn[k];
-    const int rn = r + stride;
-    if (rn < M) load_row(rn);  // the next row's loads in flight while this one is computed
-    float s = 0.0f;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (lane + 64 * k) * 4;
-      if (c < D) {
-        const f4 h = o[k];
-        o[k] = f4{elu1(h.x), elu1(h.y), elu1(h.z), elu1(h.w)};
-        s += (o[k].x + o[k].y) + (o[k].z + o[k].w);
-      } else {
-        o[k] = f4(0.0f);
-      }
-    }
-    const float mean = wave_sum(s) / (float)D;
-    float q = 0.0f;
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (lane + 64 * k) * 4;
-      if (c < D) {
-        const f4 d = o[k] - mean;
-        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
-      }
-    }
-    const float var = wave_sum(q) / (float)D + 1e-9f;
-    const float rstd = rsqrtf(var);
-    const RowDrop rd(key, (uint64_t)r * (uint64_t)D);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int c = (lane + 64 * k) * 4;
-      if (c < D) {
-        const f4 sc = *reinterpret_cast<const f4*>(scale + c);
-        const f4 of = *reinterpret_cast<const f4*>(offset + c);
-        f4 y = (o[k] - mean) * sc * rstd + of;
-        if (training) {
-          y.x = rd.keep(c + 0, dt) ? y.x * inv_keep : 0.0f;
-          y.y = rd.keep(c + 1, dt) ? y.y * inv_keep : 0.0f;
-          y.z = rd.keep(c + 2, dt) ? y.z * inv_keep : 0.0f;
-          y.w = rd.keep(c + 3, dt) ? y.w * inv_keep : 0.0f;
-        }
-        *reinterpret_cast<f4*>(Y + (int64_t)r * ldy + c) = y;
-      }
-    }
-    if (lane == 0) {
-      mean_out[r] = mean;
-      rstd_out[r] = rstd;
-    }
-    r = rn;
-  }
-}
-
 template <int NV, bool AGG>
 __global__ __launch_bounds__(256) void sage_norm_bwd_kernel(
     GradSrc src, const float* __restrict__ hB, int64_t ldb,
@@ -805,18 +721,6 @@ int gnn_sage_norm_fwd_f32(const float* hB, int64_t ldb, int64_t D1, const float*
   const int nv = (int)ceil_div(D, 256);
   hipStream_t st = (hipStream_t)stream;
   const float inv_keep = 1.0f / (1.0f - p_drop);
-  // GNN_SAGE_FWD_PIPE = G > 0: the row-walking form on at most G workgroups (experiments; 0 / unset:
-  // one row per wave)
-  int pipe = 0;
-  if (const char* e = getenv("GNN_SAGE_FWD_PIPE")) pipe = atoi(e);
-  if (pipe > 0 && nv == 4) {
-    const unsigned g = (unsigned)std::min<int64_t>(ceil_div(M, 4), pipe);
-    hipLaunchKernelGGL(sage_norm_fwd_pipe_kernel<4>, dim3(g), dim3(256), 0, st, hB ? hB : hW, ldb, biasB, (int)D1, hW,
-                       ldw, biasW, D, scale, offset, (int)M, p_drop, inv_keep, seed, training, Y, ldy, mean_out,
-                       rstd_out);
-    GNN_LAUNCHED("sage_norm_fwd_pipe_kernel");
-    return 0;
-  }
   hipLaunchKernelGGL(fwd_fn(nv), dim3((unsigned)ceil_div(M, 4)), dim3(256), 0, st, hB ? hB : hW, ldb, biasB,
                      (int)D1, hW, ldw, biasW, D, scale, offset, (int)M, p_drop, inv_keep, seed, training, Y, ldy,
                      mean_out, rstd_out);

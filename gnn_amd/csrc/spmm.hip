@@ -22,6 +22,7 @@
 //    before the FMAs (memory-level parallelism for an HBM/Infinity-Cache bound gather).
 //  * Everything is stream-ordered on the caller's stream: no host syncs, no allocation.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <hip/hip_ext.h>
 
 #include <climits>
@@ -1944,6 +1945,28 @@ int gnn_host_register(void* host, size_t bytes) {
 int gnn_host_unregister(void* host) {
   GNN_REQUIRE(host, "gnn_host_unregister: NULL");
   GNN_HIP(hipHostUnregister(host), "hipHostUnregister");
+  return 0;
+}
+
+int gnn_stream_create_cu_masked(int32_t device, int32_t cus, int32_t priority, void** stream_out) {
+  GNN_REQUIRE(stream_out, "gnn_stream_create_cu_masked: NULL stream_out");
+  *stream_out = nullptr;
+  GNN_HIP(hipSetDevice(device), "hipSetDevice");
+  int ncu = 0;
+  GNN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
+  GNN_REQUIRE(cus > 0 && cus <= ncu, "gnn_stream_create_cu_masked: cus must be in [1, %d]", ncu);
+  std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+  const int stride = ncu / cus;  // spread over the device's CU numbering (every XCD gets its share)
+  for (int i = 0, k = 0; i < ncu && k < cus; i += stride, ++k) mask[(size_t)i / 32] |= 1u << (i % 32);
+  hipStream_t st = nullptr;
+  GNN_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+  (void)priority;
+  *stream_out = (void*)st;
+  return 0;
+}
+
+int gnn_stream_destroy(void* stream) {
+  if (stream) GNN_HIP(hipStreamDestroy((hipStream_t)stream), "hipStreamDestroy");
   return 0;
 }
 

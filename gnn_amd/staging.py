@@ -150,13 +150,31 @@ def make_plan(host_batch, store: FeatureStore, rank: int, world_size: int, devic
     return StagePlan(host_batch.num_input_nodes, own_pos, own_src, host_pos, host_rows, peer_pos, peer_src, pin)
 
 
+def _staging_stream(device):
+    """The staging stream: a plain torch stream, or with GNN_STAGE_CUS = n a stream whose kernels
+    run on n of the device's CUs only (gnn_stream_create_cu_masked; experiments: the X0 gathers and
+    layer extractions then never hold LDS / wave slots on the other CUs that the step's GEMMs and
+    aggregations fill)."""
+    cus = int(os.environ.get("GNN_STAGE_CUS", "0"))
+    if cus <= 0:
+        return torch.cuda.Stream(device=device)
+    import ctypes
+
+    from . import _lib
+
+    ptr = ctypes.c_void_p()
+    idx = torch.device(device).index or 0
+    _lib.check(_lib.lib().gnn_stream_create_cu_masked(idx, cus, 0, ctypes.byref(ptr)), "gnn_stream_create_cu_masked")
+    return torch.cuda.ExternalStream(ptr.value, device=device)
+
+
 class Stager:
     """Issues X0 assembly on a side stream; ``wait`` hands X0 to the compute stream."""
 
     def __init__(self, store: FeatureStore, exchange: Optional["PeerExchange"] = None):
         self.store = store
         self.device = store.device
-        self.stream = torch.cuda.Stream(device=self.device)
+        self.stream = _staging_stream(self.device)
         self.exchange = exchange
         self.timing: Optional[list] = None  # set to [] to record (event, event, bytes) per host copy
         # optional torch.cuda.Event the staging kernels wait for (Trainer.stage_gate's event): the

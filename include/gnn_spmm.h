@@ -203,6 +203,12 @@ int gnn_ipc_export(const void* ptr, void* handle_out, int64_t* offset_out);
 int gnn_ipc_open(const void* handle, int64_t offset, int peer_device, void** ptr_out);
 int gnn_ipc_close(void* ptr, int64_t offset);
 
+/* A stream whose kernels run only on `cus` of the device's CUs, spread evenly over its CU
+ * numbering (hipExtStreamCreateWithCUMask; a blocking stream) — experiments with the X0 staging
+ * stream (GNN_STAGE_CUS). gnn_stream_destroy releases it. */
+int gnn_stream_create_cu_masked(int32_t device, int32_t cus, int32_t priority, void** stream_out);
+int gnn_stream_destroy(void* stream);
+
 /* One stream-ordered host-to-device copy (hipMemcpyAsync): the upload of a native loader's
  * batch blob (gnn_sampler.h) — every per-batch array of main.py:115-134 in one transfer. */
 int gnn_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);

@@ -95,6 +95,15 @@ def test_index_rows_matches_torch(dev):
     assert torch.equal(x.grad, ref)
 
 
+def _assert_rel_l2(got, ref, what, tol=1e-5):
+    """Norm-wise gradient check beside the elementwise one (rtol 2e-3 elementwise is
+    needed only for entries that cancel to near zero): ||got - ref|| <= tol * ||ref||."""
+    g = got.detach().cpu().double().numpy()
+    r = np.asarray(ref, dtype=np.float64)
+    rel = float(np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30))
+    assert rel <= tol, f"{what}: relative L2 error {rel:.2e} > {tol:.0e}"
+
+
 def _golden_inputs(golden, dev):
     z = golden("ladies_tiny.npz")
     adjs = [torch.sparse_coo_tensor(torch.from_numpy(z[f"c2_adj{li}_indices"]),
@@ -128,6 +137,7 @@ def test_gpu_model_step_matches_reference(dev, golden, name, fused):
     for pname, prm in net.named_parameters():
         np.testing.assert_allclose(prm.grad.cpu().numpy(), st[f"{name}_grad_{pname}"], rtol=2e-3, atol=1e-5,
                                    err_msg=pname)
+        _assert_rel_l2(prm.grad, st[f"{name}_grad_{pname}"], pname)
     torch.nn.utils.clip_grad_norm_(net.parameters(), 5)
     opt.step()
     # Adam's first step moves every weight by ~lr * sign(grad): compare where the golden
@@ -235,6 +245,7 @@ def test_gpu_forward_loss_matches_reference(dev, golden, name):
     for pname, prm in net.named_parameters():
         np.testing.assert_allclose(prm.grad.cpu().numpy(), st[f"{name}_grad_{pname}"], rtol=2e-3, atol=1e-5,
                                    err_msg=pname)
+        _assert_rel_l2(prm.grad, st[f"{name}_grad_{pname}"], pname)
 
 
 def _keep_mask_ref(seed, e, p):
@@ -304,27 +315,3 @@ def test_dropout_mask_past_2_32_elements(dev):
     assert np.array_equal(rows != 0, ref)
     assert np.all(rows[ref] == np.float32(1.0) / np.float32(0.75))
 
-
-@pytest.mark.parametrize("grid", [1, 7, 1024])
-@pytest.mark.parametrize("M,bias", [(15809, True), (1000, False), (3, True)])
-def test_sage_norm_fwd_row_walking_form_is_bit_identical(dev, monkeypatch, grid, M, bias):
-    """GNN_SAGE_FWD_PIPE=G (waves walk rows with the next row's loads in flight, on at most G
-    workgroups) against the one-row-per-wave kernel: outputs, means and rstds bit for bit, with
-    dropout (training) on."""
-    g = torch.Generator().manual_seed(M + grid)
-    hB = torch.randn(M, 512, generator=g).to(dev)
-    hW = torch.randn(M, 512, generator=g).to(dev)
-    scale = (torch.rand(1024, generator=g) + 0.5).to(dev)
-    offset = torch.randn(1024, generator=g).to(dev)
-    bB = torch.randn(512, generator=g).to(dev) if bias else None
-    bW = torch.randn(512, generator=g).to(dev) if bias else None
-    outs = []
-    for pipe in (None, str(grid)):
-        if pipe is None:
-            monkeypatch.delenv("GNN_SAGE_FWD_PIPE", raising=False)
-        else:
-            monkeypatch.setenv("GNN_SAGE_FWD_PIPE", pipe)
-        torch.manual_seed(9)
-        outs.append(sage_norm(hB, hW, scale, offset, p=0.1, training=True, biasB=bB, biasW=bW).detach())
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
