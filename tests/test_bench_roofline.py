@@ -84,3 +84,24 @@ def test_sites_from_trace():
     assert sorted(out) == ["bwd_L1", "fwd_L0", "fwd_L1", "fwd_L2"]
     assert out["fwd_L0"] == {"rocprof_avg_us": 240.0, "launches": 3, "kernel": "spmm_unit_kernel<4, 16, 1, 4, false>"}
     assert out["fwd_L2"]["rocprof_avg_us"] == 19.0 and out["bwd_L1"]["kernel"].endswith("true>")
+
+
+def test_host_report_reads_window_deltas():
+    """bench.py's host diagnostics: per-step CPU time of the training thread and of
+    the other threads, and the cgroup's busy CPUs and CFS throttling over the window."""
+    a = {"wall": 10.0, "proc_cpu": 100.0, "thread_cpu": 20.0, "cg_usage_usec": 5_000_000, "cg_nr_periods": 100,
+         "cg_nr_throttled": 3, "cg_throttled_usec": 1500}
+    b = {"wall": 10.5, "proc_cpu": 106.0, "thread_cpu": 20.5, "cg_usage_usec": 11_000_000, "cg_nr_periods": 105,
+         "cg_nr_throttled": 5, "cg_throttled_usec": 4500}
+    d = bench.host_delta(a, b)
+    r = bench.host_report(d, steps=100, workers=14)
+    assert r["trainer_thread_cpu_ms_per_step"] == 5.0 and r["other_threads_cpu_ms_per_step"] == 55.0
+    assert r["process_cpus_busy"] == 12.0 and r["sampler_workers"] == 14
+    assert r["cgroup"] == {"cpus_busy": 12.0, "periods": 5, "throttled_periods": 2, "throttled_ms": 3.0}
+    # no cgroup v2 counters (e.g. this container): the process part alone
+    r = bench.host_report(bench.host_delta({"wall": 0.0, "proc_cpu": 0.0, "thread_cpu": 0.0},
+                                           {"wall": 1.0, "proc_cpu": 2.0, "thread_cpu": 1.0}), steps=10, workers=2)
+    assert "cgroup" not in r and r["process_cpus_busy"] == 2.0
+    assert bench.host_report({}, steps=10, workers=2) is None
+    c = bench.host_counters()
+    assert {"wall", "proc_cpu", "thread_cpu"} <= set(c)
