@@ -28,6 +28,9 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+#include <xmmintrin.h>
+
 #include "gnn_sampler.h"
 #include "sampler_internal.h"
 
@@ -168,6 +171,29 @@ struct gnn_loader {
 
 namespace {
 
+bool getenv_off(const char* name) {
+  static const bool off = [name] {
+    const char* e = getenv(name);
+    return e && atoi(e) == 0;
+  }();
+  return off;
+}
+
+// One feature row (F floats) into an ld-wide row of the pinned blob, zero padded, by 16-byte
+// non-temporal stores: the blob is read once, by the copy engine, so its lines need no
+// read-for-ownership and should not evict the graph the sampler walks (the host rows are a
+// quarter of a Reddit batch's producer time). Byte-identical to memcpy + memset.
+inline void copy_row_nt(float* dst, const float* src, int64_t F, int64_t ld) {
+  int64_t c = 0;
+  for (; c + 4 <= F; c += 4)
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + c), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + c)));
+  for (; c < ld; c += 4) {
+    alignas(16) float t[4];
+    for (int k = 0; k < 4; ++k) t[k] = c + k < F ? src[c + k] : 0.0f;
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + c), _mm_load_si128(reinterpret_cast<const __m128i*>(t)));
+  }
+}
+
 // Fill the blob of one sampled batch (layout in gnn_sampler.h).
 void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batch& b) {
   const int nl = (int)ld.orders.size();
@@ -305,11 +331,24 @@ void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batc
   // the non-buffered feature rows (main.py:133), ld_x0-wide rows with zero padding
   if (ld.feat) {
     float* rows = (float*)at(bb + GNN_B_HOST_ROWS);
+    const bool nt = ld.ld_x0 % 4 == 0 && (uintptr_t)rows % 16 == 0 && !getenv_off("GNN_LOADER_NT");
+    constexpr size_t kAhead = 4;  // source rows prefetched ahead (random rows of the feature table)
     for (size_t i = 0; i < host_src.size(); ++i) {
+      if (i + kAhead < host_src.size()) {
+        const char* p = reinterpret_cast<const char*>(ld.feat + host_src[i + kAhead] * ld.ld_feat);
+        _mm_prefetch(p, _MM_HINT_T0);
+        _mm_prefetch(p + 64, _MM_HINT_T0);
+      }
       float* dst = rows + (int64_t)i * ld.ld_x0;
-      std::memcpy(dst, ld.feat + host_src[i] * ld.ld_feat, (size_t)ld.F * 4);
-      if (ld.ld_x0 > ld.F) std::memset(dst + ld.F, 0, (size_t)(ld.ld_x0 - ld.F) * 4);
+      const float* src = ld.feat + host_src[i] * ld.ld_feat;
+      if (nt) {
+        copy_row_nt(dst, src, ld.F, ld.ld_x0);
+      } else {
+        std::memcpy(dst, src, (size_t)ld.F * 4);
+        if (ld.ld_x0 > ld.F) std::memset(dst + ld.F, 0, (size_t)(ld.ld_x0 - ld.F) * 4);
+      }
     }
+    if (nt) _mm_sfence();  // the stores are visible before the batch is handed over
   }
   d[GNN_H_VERSION] = GNN_BLOB_VERSION;
   d[GNN_H_LAYERS] = nl;
