@@ -280,18 +280,22 @@ class Work {
     return scan_counts();
   }
 
-  // 16-bit counters (GNN_SAMPLER_CNT16=1): a column's count is at most the number of rows counted
+  // 16-bit counters (default; GNN_SAMPLER_CNT16=0: int32 only): a column's count is at most the
+  // number of rows counted
   // (each row of the canonical CSR holds a column once), so while fewer than 65,535 rows are
   // counted the counts fit 16 bits and the random increments hit an array half the size of cnt
   // (Reddit: 0.47 MB against 0.93 MB — inside a core's L2). The scan writes the live columns'
-  // counts into cnt, which the rest of the draw reads: the same integers, the same draw.
+  // counts into cnt, which the rest of the draw reads: the same integers, the same draw. On the
+  // box's EPYC 9575F (scripts/sampler_probe.py, one thread, Reddit): count phase 4.83 / 4.88 ms
+  // per batch against 5.38 / 5.28, the draw 10.9 / 10.8 against 11.5 / 11.2 ms, same checksums
+  // (profiles/round6/producer/).
   std::vector<uint16_t> cnt16;
   bool in16 = false;     // this call's counts are in cnt16 (live ones mirrored into cnt)
   int64_t rows16 = 0;    // rows counted into cnt16 since the last clear
   static bool cnt16_enabled() {
     static const bool on = [] {
       const char* e = getenv("GNN_SAMPLER_CNT16");
-      return e && atoi(e) != 0;
+      return !(e && atoi(e) == 0);
     }();
     return on;
   }
