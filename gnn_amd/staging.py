@@ -248,7 +248,7 @@ class Stager:
             if self.exchange is not None:
                 extra = self.exchange.exchange(plan, x0, self.store, meta)
             batch = batch_fn() if batch_fn is not None else None
-            ev = torch.cuda.Event(blocking=_BLOCKING_WAIT)
+            ev = torch.cuda.Event()
             ev.record(st)
         keep = (own_pos, own_src, host_pos, host_dev) + tuple(extra)
         if batch is not None:
@@ -257,10 +257,6 @@ class Stager:
 
 
 _EXTRACT_CHECK = os.environ.get("GNN_EXTRACT_CHECK", "step")
-# Events the training thread waits on (the staged batch's, the retirement ones) are created with
-# hipEventBlockingSync: the thread sleeps in the wait instead of spinning a CPU for ~0.9 ms of each
-# step — a CPU the batch producers share the cgroup's quota with (GNN_BLOCKING_WAIT=0: spin)
-_BLOCKING_WAIT = os.environ.get("GNN_BLOCKING_WAIT", "1") != "0"
 # X0's own-buffer and host rows in one gather launch (GNN_GATHER2=0: two launches, the round-5 form)
 _GATHER2 = os.environ.get("GNN_GATHER2", "1") != "0"
 
@@ -313,7 +309,7 @@ class Retirement:
         self.wait_s = 0.0  # host time spent waiting for the GPU (so callers can report issue cost)
 
     def retire(self, staged) -> None:
-        ev = torch.cuda.Event(blocking=_BLOCKING_WAIT)
+        ev = torch.cuda.Event()
         ev.record()
         self.q.append((ev, staged))
         while self.q and self.q[0][0].query():
