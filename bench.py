@@ -845,6 +845,7 @@ def _main(args, held):
     compute_stream = torch.cuda.Stream(device=dev, priority=hi_pri) if args.compute_priority == "high" else None
 
     step_events = [] if os.environ.get("GNN_BENCH_STEP_EVENTS") == "1" else None
+    host_trace = [] if os.environ.get("GNN_BENCH_HOST_TRACE") == "1" else None
 
     def pipeline(next_item, steps, carry=None):
         try:
@@ -927,6 +928,9 @@ def _main(args, held):
             ph[2] += t3_ - t2_
             ph[3] += t4_ - t3_
             ph[4] += t5_ - t4_
+            if host_trace is not None:  # diagnostics (GNN_BENCH_HOST_TRACE=1): per-step phases, µs
+                host_trace.append((round(1e6 * (t1_ - t0_)), round(1e6 * (t2_ - t1_)), round(1e6 * (t3_ - t2_)),
+                                   round(1e6 * (t4_ - t3_)), round(1e6 * (t5_ - t4_))))
         return loss
 
     # 12 (was 3): interleaved on one box, the driver's 20-step form 605.8 / 604.4 with 12 against
@@ -1029,6 +1033,9 @@ def _main(args, held):
     if step_events is not None:
         evs = step_events[-args.steps:] + [w1]
         log("e2e window step spans (ms): " + " ".join(f"{a.elapsed_time(b):.3f}" for a, b in zip(evs, evs[1:])))
+    if host_trace is not None:
+        log("e2e window host phases per step (us: batch_wait, step_issue, retire, producer_wait, staging_issue): "
+            + " ".join("/".join(str(v) for v in t) for t in host_trace[-args.steps:]))
     window = {"wall_ms": round(1e3 * e2e_s, 3), "compute_stream_ms": round(w0.elapsed_time(w1), 3),
               "what": "the timed end-to-end window: wall clock between the barrier + synchronize pairs, and the "
                       "step stream's span over the same steps (the rest: the staging of the batches after the "
