@@ -1047,6 +1047,7 @@ def _main(args, held):
 
     # ------------------------------------------------- GPU step over distinct pre-sampled batches
     gpu_step, roof, spmm_detail, staging_info, dp_ab, peer_ab, prefetch_ab = None, None, {}, None, None, None, None
+    gemm_ab = None
     step_batches = []
     if not args.no_gpu_step:
         nwarm = max(2, min(args.warmup, 10))
@@ -1178,6 +1179,29 @@ def _main(args, held):
                            "what": "gpu_step mini-batches/s over the same pre-sampled batches with and without the next "
                                    "batch's layer-0 aggregation issued while the gradient all-reduce runs "
                                    "(GNN_PREFETCH_L0; the flat exchange)"}
+        gemm_ab = None
+        if world == 1 and os.environ.get("GNN_BENCH_GEMM_AB", "1") == "1" and not args.unfused:
+            # the layer GEMMs on the exact-f32 MFMA kernel (GNN_GEMM_ALGO=f32) instead of split3, over
+            # the same batches, after the reported passes: how much of gpu_step the split3 route buys
+            k_[0] = nwarm
+            torch.cuda.synchronize()
+            for j in range(len(dbs)):
+                dbs[j] = None
+                if native:
+                    pre[j].host.drop_device()
+            was = os.environ.get("GNN_GEMM_ALGO")
+            os.environ["GNN_GEMM_ALGO"] = "f32"
+            try:
+                alt_s, _, _ = timed(lambda: pipeline(nxt_pre, gsteps), lead=pre_lead)
+            finally:
+                if was is None:
+                    os.environ.pop("GNN_GEMM_ALGO", None)
+                else:
+                    os.environ["GNN_GEMM_ALGO"] = was
+            gemm_ab = {"split3": round(world * gsteps / step_s, 3), "f32": round(world * gsteps / alt_s, 3),
+                       "what": "gpu_step mini-batches/s over the same pre-sampled batches with the layer GEMMs on "
+                               "split3 (bf16 matrix cores, exact three-way fp32 split; the default) and on the "
+                               "f32-input MFMA kernel (bitwise fp32 products, GNN_GEMM_ALGO=f32)"}
         peer_ab = None
         if world > 1 and direct is not None and os.environ.get("GNN_BENCH_PEER_AB", "1") == "1":
             # the other peer-row form over the same batches (direct reads of the IPC-mapped peer
@@ -1324,6 +1348,7 @@ def _main(args, held):
             "gpu_step": gpu_step,
             "dp_exchange_ab": dp_ab,
             "prefetch_l0_ab": prefetch_ab,
+            "gemm_ab": gemm_ab,
             "peer_rows_ab": peer_ab,
             "host_issue_ms_per_step_e2e": round(1e3 * e2e_issue / args.steps, 3),
             "host_cpu_ms_per_step_e2e": round(1e3 * e2e_cpu / args.steps, 3),

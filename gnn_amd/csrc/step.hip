@@ -153,23 +153,18 @@ int fork_join(Aux* a, hipStream_t from, hipStream_t to) {
 
 // GNN_STEP_GATHER=1: gather x[sampled] first even where the GEMMs could read it in place (A/B)
 bool no_index() {
-  static const bool on = [] {
-    const char* e = getenv("GNN_STEP_GATHER");
-    const char* a = getenv("GNN_GEMM_ALGO");
-    return (e && atoi(e) != 0) || (a && std::string(a) == "f32");  // the f32 kernel has no indexed form
-  }();
-  return on;
+  // read per call, as f32_gemm() below (bench.py's `gemm_ab` pass toggles GNN_GEMM_ALGO)
+  const char* e = getenv("GNN_STEP_GATHER");
+  const char* a = getenv("GNN_GEMM_ALGO");
+  return (e && atoi(e) != 0) || (a && std::string(a) == "f32");  // the f32 kernel has no indexed form
 }
 
 // GNN_GEMM_ALGO=f32: the layer GEMMs on the f32-input MFMA kernel (gnn_gemm_f32, exact fp32)
 // instead of split3 — the same routing, x[sampled] gathered (no row-indexed operands), no aux
 // stream. For the end-to-end A/B of the two kernels (gnn_amd.fused reads the same variable).
 bool f32_gemm() {
-  static const bool on = [] {
-    const char* e = getenv("GNN_GEMM_ALGO");
-    return e && std::string(e) == "f32";
-  }();
-  return on;
+  const char* e = getenv("GNN_GEMM_ALGO");  // read per call (bench.py's `gemm_ab` pass toggles it)
+  return e && std::string(e) == "f32";
 }
 
 int gemm(int ak, int bk, int64_t M, int64_t N, int64_t K, int nb, const float* const* A, int64_t lda,
