@@ -33,6 +33,8 @@ class _Cached:
 
 t0 = time.perf_counter()
 cpath = os.path.join(cache, f"{spec.name}.npz") if cache else ""
+if cache:
+    os.makedirs(cache, exist_ok=True)
 if cpath and os.path.exists(cpath) and "fastgcn" not in kinds:
     z = np.load(cpath)
     train, A = z["train"], None
