@@ -287,8 +287,9 @@ class Work {
   // (Reddit: 0.47 MB against 0.93 MB — inside a core's L2). The scan writes the live columns'
   // counts into cnt, which the rest of the draw reads: the same integers, the same draw. On the
   // box's EPYC 9575F (scripts/sampler_probe.py, one thread, Reddit): count phase 4.83 / 4.88 ms
-  // per batch against 5.38 / 5.28, the draw 10.9 / 10.8 against 11.5 / 11.2 ms, same checksums
-  // (profiles/round6/producer/).
+  // per batch against 5.38 / 5.28, the draw 10.9 / 10.8 against 11.5 / 11.2 ms; ogbn-products
+  // (2.45 M columns: 4.9 MB against 9.8 MB) 8.99 / 9.16 against 10.87 / 10.44 ms, the draw 19.7 /
+  // 19.9 against 21.0 / 20.5 ms; same checksums (profiles/round6/producer/, products/).
   std::vector<uint16_t> cnt16;
   bool in16 = false;     // this call's counts are in cnt16 (live ones mirrored into cnt)
   int64_t rows16 = 0;    // rows counted into cnt16 since the last clear
