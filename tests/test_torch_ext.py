@@ -243,3 +243,32 @@ def test_module_uses_the_builders_csr(dev):
     ref = coalesced_reference(M2, K2, full2, rowptr2, col2, nf2)
     np.testing.assert_allclose(mod.spmm_load_balance(B, X2).cpu().numpy(), torch.sparse.mm(ref, X2.cpu()).numpy(),
                                rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_module_reference_pattern_at_config2_size(dev):
+    """The reference's SparseDenseMM pattern through `import spmm` at BASELINE config-2 sizes
+    (bench.py's `dropin` shapes): forward spmm_load_balance(A, X) on the module's create_coo_tensor
+    (15.8 k x 22.2 k, ~1.8 M nonzeros, contiguous F = 602) and backward
+    spmm_load_balance(A.transpose(0, 1).coalesce(), G) (A 8.7 k x 15.8 k, ~0.86 M nonzeros,
+    F = 1024) against the C oracle, rtol / atol 1e-5."""
+    from tests.test_spmm_gpu import _config2_operand
+
+    mod = torch_ops.load()
+    rng = np.random.default_rng(77)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    M, K, F = 15809, 22176, 602
+    full, rowptr, col, nf = _config2_operand(M, K, 1.81e6, rng)
+    A = mod.create_coo_tensor(t(full), t(rowptr), t(col), t(nf), M, K)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    X = rng.standard_normal((K, F)).astype(np.float32)
+    Y = mod.spmm_load_balance(A, t(X))
+    np.testing.assert_allclose(Y.cpu().numpy(), O.spmm_f32(rowptr, ocol, oval, X), rtol=RTOL, atol=ATOL)
+    M1, K1, F1 = 8689, 15809, 1024
+    full, rowptr, col, nf = _config2_operand(M1, K1, 0.86e6, rng)
+    A1 = mod.create_coo_tensor(t(full), t(rowptr), t(col), t(nf), M1, K1)
+    ocol, oval = O.build_operand(full, rowptr, col, nf)
+    G = rng.standard_normal((M1, F1)).astype(np.float32)
+    dX = mod.spmm_load_balance(A1.transpose(0, 1).coalesce(), t(G))
+    trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K1)
+    np.testing.assert_allclose(dX.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
