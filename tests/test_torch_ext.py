@@ -271,4 +271,11 @@ def test_module_reference_pattern_at_config2_size(dev):
     G = rng.standard_normal((M1, F1)).astype(np.float32)
     dX = mod.spmm_load_balance(A1.transpose(0, 1).coalesce(), t(G))
     trp, trc, trv = O.csr_transpose(rowptr, ocol, oval, K1)
-    np.testing.assert_allclose(dX.cpu().numpy(), O.spmm_f32(trp, trc, trv, G), rtol=RTOL, atol=ATOL)
+    # 16 M outputs summed in a different order from the oracle's: a cancelling row can leave 1e-5
+    # absolute by plain fp32 rounding, so each output is held to rtol 1e-5 of its summation scale
+    # |A|·|G| (the forward error bound of a sum) as well as to atol 1e-5 everywhere but such rows.
+    got, want = dX.cpu().numpy(), O.spmm_f32(trp, trc, trv, G)
+    scale = O.spmm_f32(trp, trc, np.abs(trv), np.abs(G))
+    err = np.abs(got - want)
+    assert bool((err <= RTOL * scale + ATOL).all())
+    assert np.count_nonzero(err > RTOL * np.abs(want) + ATOL) <= 16
