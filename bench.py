@@ -469,8 +469,8 @@ def host_report(d: dict, steps: int, workers: int) -> dict:
         out["cgroup"] = {"cpus_busy": round(d["cg_usage_usec"] * 1e-6 / d["wall"], 2) if d["wall"] > 0 else None,
                          "periods": d.get("cg_nr_periods"), "throttled_periods": d.get("cg_nr_throttled"),
                          "throttled_ms": round(d.get("cg_throttled_usec", 0) * 1e-3, 3)}
-    out["what"] = ("CPU time over the timed window: the training thread (HIP's blocking waits spin, so it "
-                   "reads near the wall), the process's other threads (the sampler producers and HIP's own "
+    out["what"] = ("CPU time over the timed window: the training thread (its waits for the GPU poll and "
+                   "sleep: staging.wait_event), the process's other threads (the sampler producers and HIP's own "
                    "threads), and the cgroup's usage and CFS-quota throttling (cpu.stat)")
     return out
 

@@ -45,6 +45,39 @@ import torch
 from . import custom_sparse_ops as cso
 
 
+# The training thread's host waits on GPU events: HIP's event wait spins, also for events made
+# with hipEventBlockingSync (profiles/round6/blocking_wait/), so the thread burned a whole CPU of
+# the cgroup's quota that the batch producers share. The wait polls the event and sleeps
+# GNN_WAIT_SLEEP_US (default 20) between polls instead, with the thread's timer slack lowered to
+# 1 µs so a sleep is not rounded up to the default 50 µs; 0 restores HIP's spinning wait.
+# Measured (profiles/round6/sleep_wait/): the training thread's CPU 1.63 -> 0.70-0.90 ms per step,
+# the same rates.
+_WAIT_SLEEP_S = max(0.0, float(os.environ.get("GNN_WAIT_SLEEP_US", "20")) * 1e-6)
+_slack_set = set()
+
+
+def wait_event(ev) -> None:
+    """Block the host until `ev` (a torch.cuda.Event) has completed: spin in HIP's wait, or with
+    GNN_WAIT_SLEEP_US poll-and-sleep (see above)."""
+    if _WAIT_SLEEP_S <= 0.0:
+        ev.synchronize()
+        return
+    if ev.query():
+        return
+    import threading
+    import time
+
+    tid = threading.get_ident()
+    if tid not in _slack_set:
+        _slack_set.add(tid)
+        try:
+            ctypes.CDLL(None).prctl(29, ctypes.c_ulong(1000), 0, 0, 0)  # PR_SET_TIMERSLACK, 1 µs
+        except (OSError, AttributeError):
+            pass
+    while not ev.query():
+        time.sleep(_WAIT_SLEEP_S)
+
+
 def _host_unregister(ptr: int, device) -> None:
     from . import _lib
 
@@ -284,7 +317,7 @@ class StagedX0:
             # device count that disagrees with the host's raises before any kernel consumes the
             # operand (a host wait on the staging event, which the staged work was issued a step
             # ahead of; GNN_EXTRACT_CHECK=end defers the check to DeviceGraph.check at the end)
-            self.event.synchronize()
+            wait_event(self.event)
             b.check_extraction(self.err_host)
         cur = torch.cuda.current_stream(self._x0.device)
         cur.wait_event(self.event)
@@ -320,7 +353,7 @@ class Retirement:
             t0 = time.perf_counter()
             while len(self.q) > self.depth:
                 ev0, _ = self.q.popleft()
-                ev0.synchronize()
+                wait_event(ev0)
             self.wait_s += time.perf_counter() - t0
 
     def drain(self) -> None:

@@ -66,3 +66,28 @@ def test_prepare_data_reference_batching():
     perm = torch.randperm(len(train), generator=torch.Generator().manual_seed(4)).numpy()
     got = np.sort(np.concatenate([c[1] for c in calls]))
     assert np.array_equal(got, np.sort(train[perm[500:1000]]))
+
+
+def test_wait_event_polls_until_complete(monkeypatch):
+    """staging.wait_event: with a sleep interval it polls the event (never HIP's spinning wait)
+    until it completes; with 0 it calls synchronize()."""
+
+    class Ev:
+        def __init__(self, ready_after):
+            self.n, self.ready_after, self.synced = 0, ready_after, False
+
+        def query(self):
+            self.n += 1
+            return self.n > self.ready_after
+
+        def synchronize(self):
+            self.synced = True
+
+    monkeypatch.setattr(staging, "_WAIT_SLEEP_S", 1e-6)
+    ev = Ev(5)
+    staging.wait_event(ev)
+    assert ev.n == 6 and not ev.synced
+    monkeypatch.setattr(staging, "_WAIT_SLEEP_S", 0.0)
+    ev = Ev(5)
+    staging.wait_event(ev)
+    assert ev.synced and ev.n == 0
