@@ -983,7 +983,7 @@ def _main(args, held):
         return el, issued, out
 
     # ------------------------------------------------- headline: end to end, live sampling
-    from gnn_amd.loader import BatchLoader, NativeLoader
+    from gnn_amd.loader import BatchLoader, NativeBatch, NativeLoader, ToDevice
 
     workers = args.workers or default_workers(world)
     if args.sampler != "ladies" or args.host_extract or args.extract_layers == "none":
@@ -1010,7 +1010,9 @@ def _main(args, held):
 
     def nxt_live():
         lb = next(it)
-        return lb.plan, lambda: lb.host.to_device(dev, with_coo=False)
+        # ToDevice: Stager.issue stages a native-loader batch through one native call
+        return lb.plan, (ToDevice(lb.host, dev) if isinstance(lb.host, NativeBatch)
+                         else (lambda: lb.host.to_device(dev, with_coo=False)))
 
     # warm-up: at least the prefetch queue's depth, so the timed steps start in steady state
     # (the queue filled during setup holds pre-sampled batches that must not be timed)
@@ -1074,10 +1076,7 @@ def _main(args, held):
             j = k_[0]
             k_[0] += 1
             if native:
-                def fn(j=j):
-                    dbs[j] = pre[j].host.to_device(dev, with_coo=False)
-                    return dbs[j]
-                return pre[j].plan, fn
+                return pre[j].plan, ToDevice(pre[j].host, dev, on_built=lambda db, j=j: dbs.__setitem__(j, db))
             db = dbs[j]
             return pre[j].plan, lambda: (db.build_operands(), db)[1]
 

@@ -51,6 +51,9 @@ _SIGNATURES = {
     "gnn_host_register": (_INT, [_VP, _SZ]),
     "gnn_host_unregister": (_INT, [_VP]),
     "gnn_memcpy_h2d_async": (_INT, [_VP, _VP, _SZ, _VP]),
+    # include/gnn_stage.h
+    "gnn_stage_plan": (_SZ, [_VP, _VP]),
+    "gnn_stage_batch_f32": (_INT, [_VP, _VP]),
     "gnn_stream_create_cu_masked": (_INT, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_VP)]),
     "gnn_stream_destroy": (_INT, [_VP]),
     "gnn_ipc_export": (_INT, [_VP, _VP, ctypes.POINTER(_I64)]),

@@ -11,8 +11,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRCS = [os.path.join(HERE, "csrc", f) for f in ("spmm.hip", "sage.hip", "gemm.hip", "optim.hip", "head.hip", "extract.hip", "step.hip", "colcount.hip")]
-HDRS = [os.path.join(REPO, "include", f) for f in ("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h", "gnn_step.h")] + [
+SRCS = [os.path.join(HERE, "csrc", f) for f in ("spmm.hip", "sage.hip", "gemm.hip", "optim.hip", "head.hip", "extract.hip", "step.hip", "colcount.hip", "stage.hip")]
+HDRS = [os.path.join(REPO, "include", f) for f in ("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h", "gnn_step.h", "gnn_stage.h")] + [
     os.path.join(HERE, "csrc", "common.h")]
 OUT = os.path.join(HERE, "libgnn_spmm.so")
 ARCH = os.environ.get("GNN_OFFLOAD_ARCH", "gfx950")

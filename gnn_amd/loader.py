@@ -165,6 +165,12 @@ L_FULLROWPTR, L_ROWPTR, L_COLIDX, L_NORMFACT, L_CSC_COLPTR, L_CSC_ROWS, L_ROWS, 
     L_COLSEG = range(8, 30, 2)
 B_LABELS, B_HOST_ROWS, B_OWN_POS, B_OWN_SRC, B_HOST_POS, B_HOST_SRC, B_INPUT_NODES = range(0, 14, 2)
 KINDS = {"ladies": 0, "subgraph": 1, "fastgcn": 2}
+# include/gnn_stage.h (gnn_stage_batch_f32's argument slots and per-layer arena offsets)
+STAGE_SLOTS, STAGE_OUT_SLOTS, BLOB_MAX_LAYERS = 24, 6, 16
+(ST_DESC, ST_HOST_BLOB, ST_DEV_BLOB, ST_UPLOAD, ST_BUFFER, ST_LD_BUFFER, ST_X0, ST_LD_X0, ST_F, ST_INDPTR, ST_INDICES,
+ ST_DEGREE, ST_NUM_NODES, ST_INDPTR_T, ST_INDICES_T, ST_ERR, ST_ERR_HOST, ST_GATE, ST_CSC_FROM, ST_ARENA,
+ ST_ARENA_BYTES) = range(21)
+SO_ROWPTR, SO_COL, SO_VAL, SO_ROWS_T, SO_VAL_T = range(5)
 _I32, _I64, _F32 = np.dtype(np.int32), np.dtype(np.int64), np.dtype(np.float32)
 _TDT = {_I32: torch.int32, _I64: torch.int64, _F32: torch.float32}
 
@@ -317,6 +323,82 @@ class NativeBatch:
         b = self._bb + BLOB_BATCH_SLOTS + 4 * j
         return self._d(b, _I64), self._d(b + 2, _I64)
 
+    def stage(self, device, x0: torch.Tensor, store: "staging.FeatureStore", gate=None):
+        """The DeviceBatch of this batch, with X0's own-buffer and host rows gathered into ``x0``,
+        by ONE native call on the current stream (gnn_stage_batch_f32, include/gnn_stage.h): the
+        blob's upload (unless already on the device), [a wait for ``gate``, a torch.cuda.Event],
+        the X0 gather and every layer's operand — the library calls Stager.issue + to_device
+        make, with the same arguments (bit-identical results). Copy-mode stores only."""
+        from . import _lib
+        from .custom_sparse_ops import CsrOperand
+        from .sampler import DeviceBatch, device_graph
+
+        dev = torch.device(device)
+        desc, nl = self.desc, self.num_layers
+        lbs = [self._lb(li) for li in range(nl)]
+        on_dev = any(desc[b + L_PRESENT] and desc[b + L_ON_DEVICE] for b in lbs)
+        graph = device_graph(self.graph, dev) if on_dev else None
+        upload = self._dev is None or self._dev[0] != dev
+        blob = torch.empty(self.nbytes, dtype=torch.uint8, device=dev) if upload else self._dev[1]
+        a = np.zeros(STAGE_SLOTS, np.int64)
+        a[ST_DESC], a[ST_HOST_BLOB], a[ST_DEV_BLOB], a[ST_UPLOAD] = desc.ctypes.data, self.ptr, blob.data_ptr(), upload
+        buf = store.gpu_buffer
+        a[ST_BUFFER], a[ST_LD_BUFFER] = buf.data_ptr(), buf.stride(0)
+        a[ST_X0], a[ST_LD_X0], a[ST_F] = x0.data_ptr(), x0.stride(0), x0.shape[1]
+        err_host = None
+        if graph is not None:
+            a[ST_INDPTR], a[ST_INDICES], a[ST_DEGREE] = (graph.indptr.data_ptr(), graph.indices.data_ptr(),
+                                                         graph.degree.data_ptr())
+            a[ST_NUM_NODES], a[ST_INDPTR_T], a[ST_INDICES_T] = (graph.num_nodes, graph.indptr_t.data_ptr(),
+                                                                graph.indices_t.data_ptr())
+            a[ST_ERR] = graph.err.data_ptr()
+            # a flag of its own per build (as DeviceBatch.build_operands: ADVICE r4)
+            err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            a[ST_ERR_HOST] = err_host.data_ptr()
+        a[ST_GATE] = gate.cuda_event if gate is not None else 0  # 0 until first recorded: no wait
+        a[ST_CSC_FROM] = int(self.extra.get("csc_from", 1))
+        L = _lib.lib()
+        out = np.empty(BLOB_MAX_LAYERS * STAGE_OUT_SLOTS, np.int64)
+        nbytes = L.gnn_stage_plan(a.ctypes.data, out.ctypes.data)
+        if nbytes == 0:
+            raise RuntimeError("gnn_stage_plan: " + L.gnn_last_error().decode(errors="replace"))
+        arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        a[ST_ARENA], a[ST_ARENA_BYTES] = arena.data_ptr(), nbytes
+        with _lib.on_device(dev):
+            st = _lib.stream_of(dev)
+            _lib.check(L.gnn_stage_batch_f32(a.ctypes.data, st), "gnn_stage_batch_f32")
+            if upload:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(dev))
+                self._uploads[:] = [e for e in self._uploads if not e.query()] + [ev]
+                self._dev = (dev, blob)
+
+        def av(off, n, tdt):
+            return arena[off:off + n * 4].view(tdt)
+
+        adjs, sn = [], []
+        for li, b in enumerate(lbs):
+            x = self._d(b + L_SAMPLED, _I64)
+            if not desc[b + L_PRESENT]:
+                adjs.append(None)
+                sn.append(x)
+                continue
+            if desc[b + L_HAS_RMAP]:
+                x._gnn_rmap = self._d(b + L_RMAP, _I32)  # read by fused.SageAggregateFn's backward
+            sn.append(x)
+            M, K, nnz = int(desc[b + L_M]), int(desc[b + L_K]), int(desc[b + L_NNZ])
+            o = out[li * STAGE_OUT_SLOTS:(li + 1) * STAGE_OUT_SLOTS]
+            rowptr = av(int(o[SO_ROWPTR]), M + 1, torch.int32) if o[SO_ROWPTR] >= 0 else self._d(b + L_ROWPTR, _I32)
+            op = CsrOperand(rowptr, av(int(o[SO_COL]), nnz, torch.int32), av(int(o[SO_VAL]), nnz, torch.float32), (M, K))
+            if o[SO_VAL_T] >= 0:
+                rows_t = av(int(o[SO_ROWS_T]), nnz, torch.int32) if o[SO_ROWS_T] >= 0 else self._d(b + L_CSC_ROWS, _I32)
+                op._link(CsrOperand(self._d(b + L_CSC_COLPTR, _I32), rows_t, av(int(o[SO_VAL_T]), nnz, torch.float32),
+                                    (K, M)))
+            adjs.append(op)
+        C = int(desc[H_CLASSES])
+        labels = self._d(self._bb + B_LABELS, _F32).view(-1, C)
+        return DeviceBatch(self, None, adjs, sn, labels, graph, err_host=err_host, keep=[blob, arena])
+
     def to_device(self, device, with_coo: bool = True, build: bool = True, graph=None):
         """The DeviceBatch of this batch: views of the uploaded blob (no further copies), then
         (build=True) the operand builds / GPU extractions on the current stream."""
@@ -356,6 +438,24 @@ class NativeBatch:
         db = DeviceBatch(self, raw, None, sn, labels, graph)
         if build:
             db.build_operands(with_coo=with_coo)
+        return db
+
+
+class ToDevice:
+    """batch_fn of staging.Stager.issue for a native-loader batch: ``host.to_device(dev,
+    with_coo=False)``. Stager.issue recognises it and, when it can (copy-mode store, no copy
+    timing), stages the batch through one native call instead (NativeBatch.stage); either way
+    ``on_built`` (optional) receives the DeviceBatch."""
+
+    __slots__ = ("host", "dev", "on_built")
+
+    def __init__(self, host, dev, on_built=None):
+        self.host, self.dev, self.on_built = host, dev, on_built
+
+    def __call__(self):
+        db = self.host.to_device(self.dev, with_coo=False)
+        if self.on_built is not None:
+            self.on_built(db)
         return db
 
 

@@ -156,6 +156,9 @@ class DeviceBatch:
     # pinned host copy of the graph's extraction error flag, taken on the build stream right after
     # this batch's GPU extractions (None when no layer was extracted on the GPU)
     err_host: Optional[torch.Tensor] = None
+    # a natively staged batch (loader.NativeBatch.stage): raw is None, the operands are views of
+    # these allocations (the device blob and the staging arena)
+    keep: Optional[list] = None
 
     def check_extraction(self, err_host: Optional[torch.Tensor] = None) -> None:
         """Raise if a GPU extraction up to and including this batch's saw a device count that
@@ -170,8 +173,9 @@ class DeviceBatch:
     def tensors(self) -> list:
         """Every device tensor the step reads: CSR pieces, sampled_nodes (+ residual row
         maps), labels and the built operands (record_stream across streams)."""
-        ts = [t for r in self.raw if r is not None for t in (r[0], r[1], r[2], r[3], r[5], r[6], r[7], r[8], r[10])
-              if t is not None]
+        ts = [t for r in (self.raw or []) if r is not None
+              for t in (r[0], r[1], r[2], r[3], r[5], r[6], r[7], r[8], r[10]) if t is not None]
+        ts.extend(self.keep or [])
         for x in self.sampled_nodes:
             ts.append(x)
             if getattr(x, "_gnn_rmap", None) is not None:
@@ -186,6 +190,8 @@ class DeviceBatch:
         """create_coo_tensor for every layer (stream-ordered on the current stream)."""
         from . import custom_sparse_ops as cso
 
+        if self.raw is None:
+            raise RuntimeError("DeviceBatch: staged natively (gnn_stage_batch_f32); its operands are built")
         adjs = []
         csc_from = int(self.host.extra.get("csc_from", 1))
         for li, r in enumerate(self.raw):

@@ -244,6 +244,18 @@ class Stager:
         # uploads, so batch i+1's X0 assembles while batch i computes.
         with torch.cuda.stream(st):
             x0 = torch.empty((plan.n_input, self.store.ld), dtype=torch.float32, device=dev)
+            if _NATIVE_STAGE and plan.blob is not None and self.timing is None and not self.store.zero_copy:
+                from .loader import ToDevice
+
+                if isinstance(batch_fn, ToDevice) and batch_fn.host is plan.blob:
+                    # the native loader's batch: blob upload, X0 gather and operands in ONE call
+                    batch = plan.blob.stage(dev, x0, self.store, self.gate)
+                    if batch_fn.on_built is not None:
+                        batch_fn.on_built(batch)
+                    extra = self.exchange.exchange(plan, x0, self.store, meta) if self.exchange is not None else ()
+                    ev = torch.cuda.Event()
+                    ev.record(st)
+                    return StagedX0(x0, ev, tuple(extra) + tuple(batch.tensors()), self.store.F, batch)
             nh = len(plan.host_pos)
             if self.timing is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -292,6 +304,10 @@ class Stager:
 _EXTRACT_CHECK = os.environ.get("GNN_EXTRACT_CHECK", "step")
 # X0's own-buffer and host rows in one gather launch (GNN_GATHER2=0: two launches, the round-5 form)
 _GATHER2 = os.environ.get("GNN_GATHER2", "1") != "0"
+# a native-loader batch staged by one native call (gnn_stage_batch_f32; GNN_NATIVE_STAGE=0: the
+# Python sequence of calls, the round-5 form); it gathers X0 in one launch, so GNN_GATHER2=0 also
+# selects the Python sequence
+_NATIVE_STAGE = os.environ.get("GNN_NATIVE_STAGE", "1") != "0" and _GATHER2
 
 
 class StagedX0:

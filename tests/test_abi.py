@@ -11,7 +11,7 @@ from gnn_amd import _lib
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _declared(headers=("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h", "gnn_step.h")):
+def _declared(headers=("gnn_spmm.h", "gnn_layers.h", "gnn_optim.h", "gnn_extract.h", "gnn_step.h", "gnn_stage.h")):
     txt = ""
     for h in headers:
         with open(os.path.join(REPO, "include", h)) as f:

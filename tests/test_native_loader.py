@@ -220,3 +220,59 @@ def test_locality_sampling_leaves_the_draw_unchanged_at_scale_1():
     assert not np.array_equal(h1.input_nodes, h4.input_nodes)
     hn = sampler.ladies_sample_host(*args, skew, 1.0, [0, 1])
     _eq(h1.input_nodes, hn.input_nodes, "numpy == native at scale 1")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dx", [False, True, [1]])
+def test_native_stage_equals_python_staging(dev, dx):
+    """Stager.issue with a loader.ToDevice batch_fn stages the batch through ONE native call
+    (gnn_stage_batch_f32: blob upload, X0 gather, every layer's operand, the error flag) — X0,
+    every operand and transpose, sampled nodes, row maps and labels bit-identical to the Python
+    sequence of calls on the same batch (two loaders with the same seeds: both upload). dx=[1]:
+    layer 1 extracted on the GPU, the others built from the blob's CSR / CSC. A gate event that
+    the stream must wait for is recorded on another stream behind a delay first."""
+    lap, labels, feats, train, pl = _setup()
+    dev_of, idx_on = pl.device_id_of_nodes_group[0], pl.idx_of_nodes_on_device_group[0]
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    kw = dict(store=store, workers=2, seed=5, device_extract=dx)
+    a = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
+    b = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
+    stager = staging.Stager(store)
+    gate_stream = torch.cuda.Stream(device=dev)
+    stager.gate = torch.cuda.Event()
+    built = []
+    try:
+        for n, (pa, pb) in enumerate(zip(a.epoch(1), b.epoch(1))):
+            with torch.cuda.stream(gate_stream):
+                torch.cuda._sleep(2_000_000)  # the staging must wait for the gate, not run past it
+                stager.gate.record(gate_stream)
+            sa = stager.issue(pa.plan, lambda: pa.host.to_device(dev, with_coo=False))
+            sb = stager.issue(pb.plan, loader.ToDevice(pb.host, dev, on_built=built.append))
+            assert sb.batch.raw is None and built[-1] is sb.batch, "the native path ran"
+            xa, xb = sa.wait(), sb.wait()
+            torch.cuda.synchronize()
+            assert torch.equal(xa, xb)
+            da, db = sa.batch, sb.batch
+            assert torch.equal(da.labels, db.labels)
+            assert (da.err_host is None) == (db.err_host is None)
+            if db.err_host is not None:
+                assert int(db.err_host[0]) == 0
+            for x, y in zip(da.sampled_nodes, db.sampled_nodes):
+                assert torch.equal(x, y)
+                ra, rb = getattr(x, "_gnn_rmap", None), getattr(y, "_gnn_rmap", None)
+                assert (ra is None) == (rb is None) and (ra is None or torch.equal(ra, rb))
+            for li, (oa, ob) in enumerate(zip(sa.adjs, sb.adjs)):
+                assert oa.shape == ob.shape and oa.nnz == ob.nnz
+                for k in ("rowptr", "col", "val"):
+                    assert torch.equal(getattr(oa, k), getattr(ob, k)), (li, k)
+                assert (oa._t is None) == (ob._t is None), li
+                if oa._t is not None:
+                    for k in ("rowptr", "col", "val"):
+                        assert torch.equal(getattr(oa._t, k), getattr(ob._t, k)), (li, "t", k)
+            with pytest.raises(RuntimeError, match="staged natively"):
+                db.build_operands()
+            if n == 3:
+                break
+    finally:
+        a.close()
+        b.close()
