@@ -222,6 +222,47 @@ def test_locality_sampling_leaves_the_draw_unchanged_at_scale_1():
     _eq(h1.input_nodes, hn.input_nodes, "numpy == native at scale 1")
 
 
+def _compare_staging(a, b, store, dev, nbatches, gate=True):
+    """Batches of two NativeLoaders with the same seeds: a's through the Python sequence of staging
+    calls, b's through the one native call; everything the step reads must be bit-identical."""
+    stager = staging.Stager(store)
+    gate_stream = torch.cuda.Stream(device=dev)
+    stager.gate = torch.cuda.Event() if gate else None
+    built = []
+    for n, (pa, pb) in enumerate(zip(a.epoch(1), b.epoch(1))):
+        if gate:
+            with torch.cuda.stream(gate_stream):
+                torch.cuda._sleep(2_000_000)  # the staging must wait for the gate, not run past it
+                stager.gate.record(gate_stream)
+        sa = stager.issue(pa.plan, lambda: pa.host.to_device(dev, with_coo=False))
+        sb = stager.issue(pb.plan, loader.ToDevice(pb.host, dev, on_built=built.append))
+        assert sb.batch.raw is None and built[-1] is sb.batch, "the native path ran"
+        xa, xb = sa.wait(), sb.wait()
+        torch.cuda.synchronize()
+        assert torch.equal(xa, xb)
+        da, db = sa.batch, sb.batch
+        assert torch.equal(da.labels, db.labels)
+        assert (da.err_host is None) == (db.err_host is None)
+        if db.err_host is not None:
+            assert int(db.err_host[0]) == 0
+        for x, y in zip(da.sampled_nodes, db.sampled_nodes):
+            assert torch.equal(x, y)
+            ra, rb = getattr(x, "_gnn_rmap", None), getattr(y, "_gnn_rmap", None)
+            assert (ra is None) == (rb is None) and (ra is None or torch.equal(ra, rb))
+        for li, (oa, ob) in enumerate(zip(sa.adjs, sb.adjs)):
+            assert oa.shape == ob.shape and oa.nnz == ob.nnz
+            for k in ("rowptr", "col", "val"):
+                assert torch.equal(getattr(oa, k), getattr(ob, k)), (li, k)
+            assert (oa._t is None) == (ob._t is None), li
+            if oa._t is not None:
+                for k in ("rowptr", "col", "val"):
+                    assert torch.equal(getattr(oa._t, k), getattr(ob._t, k)), (li, "t", k)
+        with pytest.raises(RuntimeError, match="staged natively"):
+            db.build_operands()
+        if n + 1 == nbatches:
+            break
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dx", [False, True, [1]])
 def test_native_stage_equals_python_staging(dev, dx):
@@ -237,42 +278,28 @@ def test_native_stage_equals_python_staging(dev, dx):
     kw = dict(store=store, workers=2, seed=5, device_extract=dx)
     a = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
     b = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, **kw)
-    stager = staging.Stager(store)
-    gate_stream = torch.cuda.Stream(device=dev)
-    stager.gate = torch.cuda.Event()
-    built = []
     try:
-        for n, (pa, pb) in enumerate(zip(a.epoch(1), b.epoch(1))):
-            with torch.cuda.stream(gate_stream):
-                torch.cuda._sleep(2_000_000)  # the staging must wait for the gate, not run past it
-                stager.gate.record(gate_stream)
-            sa = stager.issue(pa.plan, lambda: pa.host.to_device(dev, with_coo=False))
-            sb = stager.issue(pb.plan, loader.ToDevice(pb.host, dev, on_built=built.append))
-            assert sb.batch.raw is None and built[-1] is sb.batch, "the native path ran"
-            xa, xb = sa.wait(), sb.wait()
-            torch.cuda.synchronize()
-            assert torch.equal(xa, xb)
-            da, db = sa.batch, sb.batch
-            assert torch.equal(da.labels, db.labels)
-            assert (da.err_host is None) == (db.err_host is None)
-            if db.err_host is not None:
-                assert int(db.err_host[0]) == 0
-            for x, y in zip(da.sampled_nodes, db.sampled_nodes):
-                assert torch.equal(x, y)
-                ra, rb = getattr(x, "_gnn_rmap", None), getattr(y, "_gnn_rmap", None)
-                assert (ra is None) == (rb is None) and (ra is None or torch.equal(ra, rb))
-            for li, (oa, ob) in enumerate(zip(sa.adjs, sb.adjs)):
-                assert oa.shape == ob.shape and oa.nnz == ob.nnz
-                for k in ("rowptr", "col", "val"):
-                    assert torch.equal(getattr(oa, k), getattr(ob, k)), (li, k)
-                assert (oa._t is None) == (ob._t is None), li
-                if oa._t is not None:
-                    for k in ("rowptr", "col", "val"):
-                        assert torch.equal(getattr(oa._t, k), getattr(ob._t, k)), (li, "t", k)
-            with pytest.raises(RuntimeError, match="staged natively"):
-                db.build_operands()
-            if n == 3:
-                break
+        _compare_staging(a, b, store, dev, 4)
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.gpu
+def test_native_stage_config2(dev):
+    """The same comparison at BASELINE config 2 (Reddit-shaped graph, samp 8192, batch 512, buffer
+    0.1 of the nodes, every layer extracted on the GPU, 602 features in 608-float X0 rows)."""
+    A, labels, feats, ncls, train, *_ = graphs.make_dataset(graphs.REDDIT, seed=0)
+    lap = graphs.lap_matrix(A, "graphsage")
+    N = A.shape[0]
+    pl = placement.create_buffer(lap, train, int(0.1 * N), [0], 3, alpha=0)
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], dev, 0)
+    dev_of, idx_on = pl.device_id_of_nodes_group[0], pl.idx_of_nodes_on_device_group[0]
+    kw = dict(store=store, workers=2, seed=11, device_extract=True)
+    a = loader.NativeLoader(lap, labels, train, 8192, 512, [1, 1, 1], dev_of, idx_on, **kw)
+    b = loader.NativeLoader(lap, labels, train, 8192, 512, [1, 1, 1], dev_of, idx_on, **kw)
+    try:
+        _compare_staging(a, b, store, dev, 2)
     finally:
         a.close()
         b.close()
