@@ -15,7 +15,6 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstring>
 
 #include "common.h"
 #include "gnn_extract.h"
@@ -141,6 +140,7 @@ size_t gnn_stage_plan(const int64_t* args, int64_t* out) {
 
 int gnn_stage_batch_f32(const int64_t* a, void* stream) {
   GNN_REQUIRE(a, "gnn_stage_batch_f32: NULL arguments");
+  // the layout the caller sized the arena by (gnn_stage_plan), recomputed: a few integer ops per layer
   int64_t out[GNN_BLOB_MAX_LAYERS * GNN_STAGE_OUT_SLOTS];
   const size_t need = plan(a, out);
   if (need == 0) return GNN_EINVAL;
