@@ -303,3 +303,70 @@ def test_native_stage_config2(dev):
     finally:
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("dx", [False, True, [1]])
+def test_stage_plan_layout(dx):
+    """gnn_stage_plan (host-only code of include/gnn_stage.h) on real native-loader batches: every
+    array the staging call writes gets a 256-byte-aligned, non-overlapping arena range of its
+    size; GPU-extracted layers get their row pointer (and from layer 1 their transpose's rows and
+    values), host-built layers only col / val (+ the transpose's values: the blob holds its CSC);
+    the extraction workspace exists iff a layer is extracted and is large enough for each; a
+    descriptor of another blob version is refused with a message."""
+    from gnn_amd import _lib
+
+    lap, labels, feats, train, pl = _setup()
+    dev_of, idx_on = pl.device_id_of_nodes_group[0], pl.idx_of_nodes_on_device_group[0]
+    store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], "cpu", 0)
+    b = loader.NativeLoader(lap, labels, train, 400, 96, [1, 1, 1], dev_of, idx_on, store=store, workers=2, seed=4,
+                            device_extract=dx)
+    L = _lib.lib()
+    try:
+        lb = next(iter(b.epoch(1)))
+        nb = lb.host
+        a = np.zeros(loader.STAGE_SLOTS, np.int64)
+        a[loader.ST_DESC], a[loader.ST_HOST_BLOB] = nb.desc.ctypes.data, nb.ptr
+        a[loader.ST_NUM_NODES], a[loader.ST_CSC_FROM] = lap.shape[0], 1
+        out = np.full(loader.BLOB_MAX_LAYERS * loader.STAGE_OUT_SLOTS, -7, np.int64)
+        nbytes = L.gnn_stage_plan(a.ctypes.data, out.ctypes.data)
+        assert nbytes > 0 and nbytes % 256 == 0
+        ranges = []
+        any_dev = False
+        for li in range(nb.num_layers):
+            base = nb._lb(li)
+            o = out[li * loader.STAGE_OUT_SLOTS:(li + 1) * loader.STAGE_OUT_SLOTS]
+            M, K, nnz = (int(nb.desc[base + s]) for s in (loader.L_M, loader.L_K, loader.L_NNZ))
+            on_dev = bool(nb.desc[base + loader.L_ON_DEVICE])
+            sizes = {loader.SO_COL: 4 * nnz, loader.SO_VAL: 4 * nnz}
+            if on_dev:
+                any_dev = True
+                sizes[loader.SO_ROWPTR] = 4 * (M + 1)
+                if li >= 1:
+                    sizes[loader.SO_ROWS_T] = sizes[loader.SO_VAL_T] = 4 * nnz
+                else:
+                    assert o[loader.SO_ROWS_T] == -1 and o[loader.SO_VAL_T] == -1
+                rt = int(nb._h(base + loader.L_FULLROWPTR, np.dtype(np.int32))[M])
+                ct = int(nb._h(base + loader.L_COLSEG, np.dtype(np.int32))[K]) if li >= 1 else 0
+                ws = L.gnn_ladies_extract_workspace_bytes(lap.shape[0], M, K, int(li >= 1), rt, ct)
+                assert out[5] >= 0 and out[5] + ws <= nbytes
+            else:
+                assert o[loader.SO_ROWPTR] == -1 and o[loader.SO_ROWS_T] == -1
+                if nb._count(base + loader.L_CSC_COLPTR) > 0:
+                    sizes[loader.SO_VAL_T] = 4 * nnz
+            for k, sz in sizes.items():
+                off = int(o[k])
+                assert off >= 0 and off % 256 == 0 and off + sz <= nbytes, (li, k, off, sz)
+                ranges.append((off, off + max(sz, 1)))
+        if any_dev:
+            ranges.append((int(out[5]), nbytes))
+        else:
+            assert out[5] == -1
+        ranges.sort()
+        assert all(e0 <= s1 for (_, e0), (s1, _) in zip(ranges, ranges[1:])), "arena ranges overlap"
+        d2 = nb.desc.copy()
+        d2[loader.H_VERSION] = 99
+        a[loader.ST_DESC] = d2.ctypes.data
+        assert L.gnn_stage_plan(a.ctypes.data, out.ctypes.data) == 0
+        assert b"version" in L.gnn_last_error()
+    finally:
+        b.close()
