@@ -2,18 +2,22 @@
 
 Headline `value` = END-TO-END mini-batches/s, as the reference's training loop runs
 (main.py:115-170): every timed step takes a batch LIVE from the sampler pool (the native
-LADIES sampler + the host gather of the non-buffered feature rows, in worker threads; the
-reference's prepare_data thread pool, sampler.py:163-193), stages X0 (own-GPU buffer gather,
-pinned host rows H2D on a side stream, peer rows by RCCL all-to-all when N > 1, the per-step
-peer negotiation included), builds the operands, and runs 3 HIP aggregation forwards + 2
-backwards inside GraphSAGE (samp_num 8192, batch 512, nhid 512, orders 1,1,1, F = 602, 41
-classes), loss, backward, clip_grad_norm_(5), RCCL all-reduce(SUM) of the flat gradient, Adam.
-The warm-up drains the sampler's prefetch queue first, so the timed steps run in steady
-state (nothing pre-sampled is consumed inside the timed region).
+LADIES sampler + the host gather of the non-buffered feature rows, in C++ worker threads; the
+reference's prepare_data thread pool, sampler.py:163-193), stages it (one native call: the
+batch blob's H2D on a side stream, X0 from the own-GPU buffer and the host rows, the lower
+layers extracted on the GPU, the operands; peer rows read from the peers' mapped buffers when
+N > 1), and runs 3 HIP aggregation forwards + 2 backwards inside GraphSAGE (samp_num 8192,
+batch 512, nhid 512, orders 1,1,1, F = 602, 41 classes), loss, backward, clip_grad_norm_(5),
+RCCL all-reduce(SUM) of the flat gradient, Adam. The warm-up drains the sampler's prefetch
+queue first, so the timed steps run in steady state (nothing pre-sampled is consumed inside
+the timed region).
 
 Second figure `gpu_step`: the same step over DISTINCT pre-sampled batches (one per timed
-step, none cycled) whose CSR pieces are resident in HBM — the GPU side alone. The SpMM
-roofline comes from that run (HIP events on the launch stream around every aggregation).
+step, none cycled), each blob uploaded afresh inside the timed region — the GPU side without
+the producers. The SpMM roofline comes from that batch set (HIP events on the launch stream
+around every aggregation, PMC counters in child processes). The line also carries where the
+host's time went (`host_cpu_e2e`, `host_phases_ms_per_step_e2e`), the drop-in boundary per call
+(`dropin`) and the split3-vs-exact-f32 GEMM A/B (`gemm_ab`); DESIGN.md §5.
 
 Synthetic Reddit-shaped graph: Chung-Lu lognormal sigma 1.3, N = 232,965,
 ~23.1 M nnz, N(0,1) fp32 features (StandardScaler'd analogue), buffer_size = 0.1.
