@@ -103,11 +103,12 @@ def parse():
                     help="LADIES: bottom-up layers (below the top one) whose sub-graph the GPU extracts "
                          "(gnn_ladies_extract_f32) instead of the sampler threads: comma list, 'all' or 'none'")
     ap.add_argument("--host-extract", action="store_true", help="= --extract-layers none")
-    ap.add_argument("--column-counts", default="auto", choices=["auto", "host", "gpu"],
-                    help="LADIES draw: U's column counts summed by the sampler threads (host) or on the GPU "
-                         "(gnn_colcount_*, the graph resident in HBM); the draw itself stays on the host. auto: "
-                         "gpu from 1 M nodes (A/B on one box: ogbn-products-shaped 363 -> 720 mini-batches/s end "
-                         "to end; Reddit-shaped 558 host vs 516 gpu, where the host draw is not the bound)")
+    ap.add_argument("--column-counts", default="auto", choices=["auto", "host", "gpu", "mixed"],
+                    help="LADIES draw: U's column counts summed by the sampler threads (host), on the GPU "
+                         "(gnn_colcount_*, the graph resident in HBM), or mixed (half the sampler threads on "
+                         "the GPU, on hardware queues of their own, the rest on the host); the draw itself "
+                         "stays on the host. auto: mixed from 1 M nodes, host below (profiles/round6/"
+                         "mixed_counts/; Reddit-shaped: the host draw is not the bound)")
     ap.add_argument("--peer-rows", default=os.environ.get("GNN_PEER_ROWS", "direct"), choices=["alltoall", "direct"],
                     help="N > 1: peer feature rows read directly from the peers' buffers over xGMI (IPC-mapped "
                          "once; default, falls back to alltoall if any rank cannot map) or by an RCCL all-to-all "
@@ -997,9 +998,13 @@ def _main(args, held):
     else:
         dx = [int(v) for v in args.extract_layers.split(",") if v]
     lkw = {}
-    counts_on_gpu = args.column_counts == "gpu" or (args.column_counts == "auto" and N >= 1_000_000)
-    if counts_on_gpu and args.sampler == "ladies" and not args.python_loader:
+    counts = args.column_counts
+    if counts == "auto":
+        counts = "mixed" if N >= 1_000_000 else "host"
+    if counts in ("gpu", "mixed") and args.sampler == "ladies" and not args.python_loader:
         lkw["device_count"] = dev
+        if counts == "mixed":
+            lkw["device_count_workers"] = max(1, workers // 2)
     loader = (BatchLoader if args.python_loader else NativeLoader)(
         lap, labels, train, args.samp_num, args.batch_size, [1, 1, 1], pdev, pidx, rank=rank, world_size=world,
         store=store, workers=workers, seed=4242, kind=args.sampler, device_extract=dx,
@@ -1345,7 +1350,9 @@ def _main(args, held):
                        "sampler_workers_per_rank": workers, "host_cpus": "gpu numa node" if len(numa_cpus) >= 4 else "all",
                        "batch_producer": "python threads" if args.python_loader else "native (C++ threads, one blob)",
                        "layer_extraction": ("gpu: layers " + args.extract_layers + "; host: the rest") if dx else "host",
-                       "column_counts": "gpu" if getattr(loader, "device_count", False) else "host"},
+                       "column_counts": (("gpu" if not getattr(loader, "device_count_workers", 0) else
+                                          f"mixed ({loader.device_count_workers} of {workers} sampler threads on "
+                                          "the GPU)") if getattr(loader, "device_count", False) else "host")},
             "roofline": roof,
             "cpu_baseline": cpu,
             "gpu_step": gpu_step,

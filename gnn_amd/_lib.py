@@ -90,6 +90,7 @@ _SIGNATURES = {
     "gnn_colcount_add": (_INT, [_VP, _VP, _I64, ctypes.POINTER(_I64), ctypes.POINTER(_VP), ctypes.POINTER(_VP)]),
     "gnn_colcount_reset": (_INT, [_VP]),
     "gnn_colcount_destroy": (None, [_VP]),
+    "gnn_colcount_set_cus": (_INT, [ctypes.c_int32]),
     "gnn_ladies_extract_f32": (_INT, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64,
                                       _I64, _VP, _VP, _VP, _VP, _VP, _VP, _SZ, _VP, _VP]),
     # include/gnn_step.h
@@ -134,6 +135,7 @@ _SAMPLER_SIGNATURES = {
                                 ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "gnn_loader_submit": (_INT, [_VP, ctypes.c_uint32, _VP, _I64]),
     "gnn_loader_set_colcount": (_INT, [_VP, _VP]),
+    "gnn_loader_set_colcount_workers": (_INT, [_VP, ctypes.c_int32]),
     "gnn_ladies_sample_cc": (_INT, [_VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, ctypes.c_int32, ctypes.c_uint32,
                                     ctypes.c_int32, _VP, _VP, ctypes.POINTER(_VP)]),
     "gnn_loader_next": (_INT, [_VP, ctypes.POINTER(_VP)]),

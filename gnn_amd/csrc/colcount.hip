@@ -33,6 +33,8 @@
 // INT32_MAX): a call of 2^31 or more entries runs the atomic form instead of wrapping an offset.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <climits>
 #include <cstdint>
@@ -43,6 +45,9 @@
 
 #include "common.h"
 #include "gnn_extract.h"
+
+// gnn_colcount_set_cus: the CU mask of the streams of contexts created from now on (0: plain)
+static std::atomic<int> g_cc_cus{0};
 
 namespace {
 
@@ -390,6 +395,12 @@ int part_grid(int64_t n) {
 
 extern "C" {
 
+int gnn_colcount_set_cus(int32_t cus) {
+  GNN_REQUIRE(cus >= 0, "gnn_colcount_set_cus: cus must be >= 0");
+  g_cc_cus.store(cus);
+  return 0;
+}
+
 int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx) {
   GNN_REQUIRE(ctx != nullptr, "gnn_colcount_create: ctx is NULL");
   *ctx = nullptr;
@@ -409,11 +420,12 @@ int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr
   // (~1.2 ms of kernels and copies per batch) then take more of the GPU from the step and the rate
   // drops 453-470 -> 404-436 (profiles/round5/configs/, r5ah, r5an) — so by default (0) the streams
   // are plain ones.
-  int cus = 0;
+  int cus = g_cc_cus.load();
   if (const char* e = getenv("GNN_CC_CUS")) cus = atoi(e);
   int ncu = 0;
   GNN_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
-  if (cus > 0 && cus <= ncu) {
+  if (cus > ncu) cus = ncu;
+  if (cus > 0) {
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     const int stride = ncu / cus;
     for (int i = 0, k = 0; i < ncu && k < cus; i += stride, ++k) mask[(size_t)i / 32] |= 1u << (i % 32);

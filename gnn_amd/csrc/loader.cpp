@@ -155,6 +155,7 @@ struct gnn_loader {
   int32_t kind, device_extract, csc_from;
   const double* fastgcn_p;
   gnn_colcount_api cc{};  // device column counting (cc.add == NULL: on the host)
+  int cc_workers = 0;     // workers 0 .. cc_workers-1 count on the device (0: all)
   // machinery
   std::shared_ptr<Pool> pool;
   std::vector<std::thread> threads;
@@ -165,8 +166,8 @@ struct gnn_loader {
   uint64_t next_id = 0, next_out = 0;
   bool stop = false;
 
-  void run();
-  gnn_batch* produce(const Job& job, void** cc_ctx);
+  void run(int worker);
+  gnn_batch* produce(const Job& job, void** cc_ctx, bool device_counts);
 };
 
 namespace {
@@ -364,13 +365,13 @@ void fill(gnn_loader& ld, const gnn_ladies_result& res, const Job& job, gnn_batc
 
 }  // namespace
 
-gnn_batch* gnn_loader::produce(const Job& job, void** cc_ctx) {
+gnn_batch* gnn_loader::produce(const Job& job, void** cc_ctx, bool device_counts) {
   std::unique_ptr<gnn_batch> b(new gnn_batch());
   b->id = job.id;
   gnn_ladies_result* res = nullptr;
   const int nl = (int)orders.size();
   int rc = 0;
-  const bool use_cc = cc.add != nullptr && kind == GNN_SAMPLER_LADIES;
+  const bool use_cc = device_counts && cc.add != nullptr && kind == GNN_SAMPLER_LADIES;
   if (use_cc && !*cc_ctx) {  // this worker's context, made on its first batch
     rc = cc.create(cc.device, N, cc.indptr, cc.indices, cc_ctx);
     if (rc != 0) {
@@ -404,7 +405,7 @@ gnn_batch* gnn_loader::produce(const Job& job, void** cc_ctx) {
   return b.release();
 }
 
-void gnn_loader::run() {
+void gnn_loader::run(int worker) {
   void* cc_ctx = nullptr;
   struct Close {
     gnn_loader* ld;
@@ -422,7 +423,11 @@ void gnn_loader::run() {
       job = std::move(jobs.front());
       jobs.pop_front();
     }
-    gnn_batch* b = produce(job, &cc_ctx);
+    // gnn_loader_set_colcount_workers (read after the job: set before the first submission;
+    // GNN_CC_WORKERS overrides for experiments)
+    int k = cc_workers;
+    if (const char* e = getenv("GNN_CC_WORKERS")) k = atoi(e);
+    gnn_batch* b = produce(job, &cc_ctx, k <= 0 || worker < k);
     {
       std::lock_guard<std::mutex> lk(mu);
       done[b->id] = b;
@@ -476,7 +481,7 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
     ld->csc_from = csc_from;
     ld->fastgcn_p = fastgcn_p;
     ld->pool.reset(new Pool(pinned != 0));
-    for (int i = 0; i < workers; ++i) ld->threads.emplace_back([p = ld.get()] { p->run(); });
+    for (int i = 0; i < workers; ++i) ld->threads.emplace_back([p = ld.get(), i] { p->run(i); });
     return ld.release();
   } catch (const std::exception& e) {
     gnn_smp::set_error(std::string("gnn_loader_create: ") + e.what());
@@ -496,6 +501,20 @@ int gnn_loader_set_colcount(gnn_loader* ld, const gnn_colcount_api* api) {
     return -22;
   }
   ld->cc = *api;
+  return 0;
+}
+
+int gnn_loader_set_colcount_workers(gnn_loader* ld, int32_t workers) {
+  if (!ld || workers < 0) {
+    gnn_smp::set_error("gnn_loader_set_colcount_workers: bad arguments");
+    return -22;
+  }
+  std::lock_guard<std::mutex> lk(ld->mu);
+  if (ld->next_id != 0) {
+    gnn_smp::set_error("gnn_loader_set_colcount_workers: batches already submitted");
+    return -22;
+  }
+  ld->cc_workers = workers;
   return 0;
 }
 

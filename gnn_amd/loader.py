@@ -470,9 +470,12 @@ class NativeLoader:
                  store: Optional[staging.FeatureStore] = None, workers: int = 8, prefetch: int = 0,
                  seed: int = 0, devices=None, kind: str = "ladies", device_extract=False,
                  pinned: Optional[bool] = None, device_count=None, skewed_sampling_nodes=None,
-                 scale_factor: float = 1.0):
+                 scale_factor: float = 1.0, device_count_workers: Optional[int] = None):
         """device_count (LADIES, a graph without stored zeros): a torch device — the workers sum
         U's column counts on it (gnn_colcount_*, the graph resident there) instead of on the host.
+        device_count_workers = k (0 < k < workers): only k of the workers count on the device, the
+        others on the host, and the device contexts get hardware queues of their own
+        (gnn_loader_set_colcount_workers, gnn_colcount_set_cus); the batches are the same.
         skewed_sampling_nodes (--locality_sampling, preprocess.py:414-423) are accepted at the
         reference's scale_factor 1.0 (main.py:256), where they leave the draw unchanged
         (sampler.py:119-121); scale_factor > 1 is the numpy branch (BatchLoader)."""
@@ -531,10 +534,17 @@ class NativeLoader:
         if not self.handle:
             raise RuntimeError("gnn_loader_create failed: " + L.gnn_sampler_last_error().decode(errors="replace"))
         self.device_count = device_count is not None and kind == "ladies" and g.data is None
+        self.device_count_workers = 0
         if self.device_count:
             self._keep["cc"] = smp.colcount_api(g, device_count)
             _lib.check_sampler(L.gnn_loader_set_colcount(self.handle, ctypes.byref(self._keep["cc"])),
                                "gnn_loader_set_colcount")
+            k = int(device_count_workers or 0)
+            if 0 < k < self.workers:
+                _lib.check_sampler(L.gnn_loader_set_colcount_workers(self.handle, k), "gnn_loader_set_colcount_workers")
+                # the counting streams off the step's hardware queues (contexts are made on first use)
+                _lib.check(_lib.lib().gnn_colcount_set_cus(65535), "gnn_colcount_set_cus")
+                self.device_count_workers = k
         self._pending = 0
 
     def _submit(self, nodes) -> None:

@@ -85,6 +85,11 @@ int gnn_ladies_extract_f32(const int64_t* indptr, const int32_t* indices, const 
  * A call's entry total is carried in int64; a call of 2^31 or more entries (beyond the int32
  * partition offsets) runs the atomic form instead. */
 int gnn_colcount_create(int32_t device, int64_t num_nodes, const int64_t* indptr, const int32_t* indices, void** ctx);
+/* The stream of the contexts created after this call (process-wide): cus = 0 a plain stream
+ * (default), cus > 0 a stream over that many CUs (>= the device's: all of them) — a CU-masked
+ * stream gets a hardware queue of its own instead of sharing one with the training step's streams
+ * (GPU_MAX_HW_QUEUES is 4). GNN_CC_CUS, when set, overrides. Returns 0, or -22 for cus < 0. */
+int gnn_colcount_set_cus(int32_t cus);
 int gnn_colcount_add(void* ctx, const int64_t* rows, int64_t n, int64_t* nlive, const uint64_t** bits,
                      const int32_t** counts);
 int gnn_colcount_reset(void* ctx);

@@ -196,6 +196,12 @@ gnn_loader* gnn_loader_create(const int64_t* indptr, const int32_t* indices, con
 /* LADIES loaders: count U's columns on the device (each worker thread makes its own context on
  * first use). Call before the first gnn_loader_submit; api is copied. */
 int gnn_loader_set_colcount(gnn_loader* ld, const gnn_colcount_api* api);
+/* With gnn_loader_set_colcount: only worker threads 0 .. workers-1 count on the device, the others
+ * on the host (0 = all of them; the batches are the same either way: the counts are exact). Device
+ * counts cost the GPU ~1.2 ms per ogbn-products-sized batch beside the step, host counts ~9 ms of a
+ * worker's CPU: a mix keeps both the GPU and the producers below their bound. GNN_CC_WORKERS, when
+ * set, overrides. Call before the first gnn_loader_submit. */
+int gnn_loader_set_colcount_workers(gnn_loader* ld, int32_t workers);
 /* Queue one batch (node ids copied); batches come out of gnn_loader_next in submission order. */
 int gnn_loader_submit(gnn_loader* ld, uint32_t seed, const int64_t* nodes, int64_t n);
 /* Block until the oldest submitted batch is ready. On a sampling error returns its status (the

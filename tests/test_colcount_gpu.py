@@ -130,7 +130,11 @@ def test_sampler_with_device_counts_equals_host(dev, gname, orders, samp, bs, dx
         cc.close()
 
 
-def test_native_loader_with_device_counts(dev):
+@pytest.mark.parametrize("cc_workers", [None, 1, 2])
+def test_native_loader_with_device_counts(dev, cc_workers):
+    """The native producer with U's column counts on the GPU — in every worker, or (cc_workers)
+    in the first k of 3 workers with the rest counting on the host, the device contexts on
+    CU-masked streams of their own (bench.py's `mixed`) — yields the host-counting batches."""
     lap = _graph("symmetric")
     N = lap.shape[0]
     rng = np.random.default_rng(3)
@@ -143,8 +147,9 @@ def test_native_loader_with_device_counts(dev):
     store = staging.FeatureStore(feats, pl.gpu_buffer_group[0], "cpu", 0)
     kw = dict(store=store, workers=3, seed=4, device_extract=True)
     a = loader.NativeLoader(lap, labels, train, 1500, 128, [1, 1, 1], dev_of, idx_on, **kw)
-    b = loader.NativeLoader(lap, labels, train, 1500, 128, [1, 1, 1], dev_of, idx_on, device_count=dev, **kw)
-    assert b.device_count
+    b = loader.NativeLoader(lap, labels, train, 1500, 128, [1, 1, 1], dev_of, idx_on, device_count=dev,
+                            device_count_workers=cc_workers, **kw)
+    assert b.device_count and b.device_count_workers == (cc_workers or 0)
     try:
         for n, (pa, pb) in enumerate(zip(a.epoch(1), b.epoch(1))):
             _same(pa.host, pb.host)
@@ -153,3 +158,4 @@ def test_native_loader_with_device_counts(dev):
     finally:
         a.close()
         b.close()
+        _lib.lib().gnn_colcount_set_cus(0)  # process-wide: later tests get plain streams again

@@ -370,3 +370,22 @@ def test_stage_plan_layout(dx):
         assert b"version" in L.gnn_last_error()
     finally:
         b.close()
+
+
+def test_set_colcount_workers_contract():
+    """gnn_loader_set_colcount_workers: a negative count is refused, and so is any call once a
+    batch has been submitted (the workers read it per batch)."""
+    from gnn_amd import _lib
+
+    lap, labels, feats, train, pl = _setup()
+    b = loader.NativeLoader(lap, labels, train, 100, 16, [1, 1], pl.device_id_of_nodes_group[0],
+                            pl.idx_of_nodes_on_device_group[0], workers=2)
+    L = _lib.sampler_lib()
+    try:
+        assert L.gnn_loader_set_colcount_workers(b.handle, -1) != 0
+        assert L.gnn_loader_set_colcount_workers(b.handle, 1) == 0
+        next(iter(b.epoch(1)))
+        assert L.gnn_loader_set_colcount_workers(b.handle, 1) != 0
+        assert b"already submitted" in L.gnn_sampler_last_error()
+    finally:
+        b.close()
