@@ -474,7 +474,7 @@ class NativeLoader:
         """device_count (LADIES, a graph without stored zeros): a torch device — the workers sum
         U's column counts on it (gnn_colcount_*, the graph resident there) instead of on the host.
         device_count_workers = k (0 < k < workers): only k of the workers count on the device, the
-        others on the host, and the device contexts get hardware queues of their own
+        others on the host, and the device contexts get hardware queues of their own on 64 CUs
         (gnn_loader_set_colcount_workers, gnn_colcount_set_cus); the batches are the same.
         skewed_sampling_nodes (--locality_sampling, preprocess.py:414-423) are accepted at the
         reference's scale_factor 1.0 (main.py:256), where they leave the draw unchanged
@@ -542,8 +542,11 @@ class NativeLoader:
             k = int(device_count_workers or 0)
             if 0 < k < self.workers:
                 _lib.check_sampler(L.gnn_loader_set_colcount_workers(self.handle, k), "gnn_loader_set_colcount_workers")
-                # the counting streams off the step's hardware queues (contexts are made on first use)
-                _lib.check(_lib.lib().gnn_colcount_set_cus(65535), "gnn_colcount_set_cus")
+                # the counting streams off the step's hardware queues, on 64 of the CUs (contexts are
+                # made on first use). Products, interleaved: 64 CUs 631 / 631 / 640 / 574 and 521 /
+                # 596 / 583 / 642 / 640 end to end, 32 CUs 636 / 637 / 500 / 461, 128 CUs 636 / 641 /
+                # 597 / 538, all CUs 483 / 636 / 483 / 567 / 627 (profiles/round6/mixed_counts/)
+                _lib.check(_lib.lib().gnn_colcount_set_cus(64), "gnn_colcount_set_cus")
                 self.device_count_workers = k
         self._pending = 0
 
